@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X linearizability checker (BASELINE.json metric: history ops
+verified/sec + configs explored/sec, % of the HBM roofline).
+
+One "step" = one full check of the workload's histories by the HIP search (lc_plan_run on
+HBM-resident encoded histories). Default workload: C3 (jepsen.independent cas-register,
+1k keys x 1k ops, 5 clients/key, p_info 0.01), the north_star's headline config; under
+`torchrun --nproc-per-node N` every rank checks its own 1k-key shard (weak scaling,
+no data-path collective: keys are independent, SURVEY §8(e) axis 1).
+
+Prints ONE JSON line on rank 0 (driver contract) with `roofline` and `cpu_baseline`.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "jepsen-jgroups-raft_amd"))
+
+from lincheck import _lib, synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+MODEL_OF = {"c1": "cas-register", "c2": "cas-register", "c3": "cas-register",
+            "c4": "cas-register", "c5": "counter"}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(h, model: str, budget_s: float, threads: int):
+    """Time the CPU oracle (a C restatement of knossos.linear, test infrastructure) on a
+    bounded sample of the same workload; returns (cpu dict, oracle results, sample keys)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (bench cpu_baseline leg only)
+    n = h.n_hist
+    if n > 1:
+        probe = list(range(min(n, threads)))
+        t0 = time.perf_counter()
+        oracle.check_many(model, h.select(probe), n_threads=threads)
+        dt = max(time.perf_counter() - t0, 1e-3)  # one key per thread ~ per-key latency
+        keys = max(threads, min(n, int(budget_s / dt * threads)))
+        sample = list(range(keys))
+        hs = h.select(sample)
+        t0 = time.perf_counter()
+        res = oracle.check_many(model, hs, n_threads=threads)
+        wall = time.perf_counter() - t0
+        desc = f"first {keys} of {n} keys, {threads} threads (one key per thread)"
+        used = threads
+    else:
+        # one history: the oracle is single-threaded like Knossos's per-history search;
+        # time a prefix of the history that fits the budget
+        frac = 1.0
+        while True:
+            m = int(h.n * frac)
+            hs = synth.truncate(h, m) if frac < 1.0 else h
+            t0 = time.perf_counter()
+            res = oracle.check_many(model, hs, n_threads=1, max_configs=0)
+            wall = time.perf_counter() - t0
+            if wall <= budget_s * 1.5 or frac < 0.01:
+                break
+            frac *= max(0.05, budget_s / wall * 0.8)
+        sample = [0]
+        desc = f"first {hs.n} of {h.n} entries of the single history, 1 thread"
+        used = 1
+    ops = hs.n_ops()
+    return ({"value": ops / wall, "unit": "history ops/s", "cores": used, "kind": "port",
+             "sample": desc, "wall_s": round(wall, 3),
+             "configs_per_s": sum(r["explored"] for r in res) / wall}, res, sample, hs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c3", choices=sorted(MODEL_OF))
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests)")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 PMC passes (or absent)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+        dist = (torch, tdist)
+
+    def barrier_sync():
+        if dist:
+            dist[0].cuda.synchronize()
+            dist[1].barrier()
+            dist[0].cuda.synchronize()
+
+    model = MODEL_OF[args.workload]
+    kind = _lib.MODEL_KIND[model]
+    cfg = synth.CONFIGS[args.workload]
+    # weak scaling: rank r checks keys [r*K, (r+1)*K) (distinct seeds per key)
+    n_keys = cfg["n_keys"] if cfg["n_keys"] == 1 else max(1, int(cfg["n_keys"] * args.scale))
+    t0 = time.perf_counter()
+    h = synth.gen_config(args.workload, key0=rank * n_keys, scale=args.scale)
+    gen_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    plan = _lib.Plan(kind, 0, h, device=local)
+    plan_s = time.perf_counter() - t0
+    log(f"[rank {rank}] {args.workload}: {h.n_hist} histories, {h.n} entries, "
+        f"{h.n_ops()} ops; gen {gen_s:.2f}s, encode+upload {plan_s:.2f}s")
+
+    for _ in range(args.warmup):
+        plan.run()
+    barrier_sync()
+    kernel_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.run()
+        kernel_ms += plan.stats()["kernel_ms"]
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        torch, tdist = dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res = plan.results()
+    st = plan.stats()
+    ops_rank = h.n_ops()
+    explored_rank = int(res["explored"].sum())
+    total_ops = ops_rank * world * args.steps
+    total_cfg = explored_rank * world * args.steps
+    value = total_ops / elapsed
+    vcount = {int(v): int((res["valid"] == v).sum()) for v in (0, 1, 2)}
+
+    if rank != 0:
+        if dist:
+            dist[1].destroy_process_group()
+        return
+
+    avg_kernel_s = kernel_ms / args.steps / 1e3
+    alg_bytes = st["alg_bytes"]  # per launch set (one step)
+    achieved = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tr = json.load(open(args.traffic))
+            if tr.get("workload") == args.workload and abs(tr.get("scale", 1.0) - args.scale) < 1e-9:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+
+    cpu = None
+    parity = None
+    if not args.no_cpu and world == 1:
+        threads = min(16, os.cpu_count() or 1)
+        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, threads)
+        if h.n_hist > 1:
+            mism = [k for i, k in enumerate(sample)
+                    if int(res["valid"][k]) != ores[i]["valid"] or
+                    int(res["fail_idx"][k]) != ores[i]["fail_idx"] or
+                    int(res["explored"][k]) != ores[i]["explored"]]
+            parity = {"keys_compared": len(sample), "mismatches": len(mism)}
+        else:
+            g = _lib.check(kind, 0, hs)
+            parity = {"keys_compared": 1,
+                      "mismatches": int(int(g["valid"][0]) != ores[0]["valid"] or
+                                        int(g["explored"][0]) != ores[0]["explored"])}
+
+    out = {
+        "metric": "history ops verified/sec (+ configs explored/sec, % HBM roofline)",
+        "value": value,
+        "unit": "history ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (simulated linearizable SUT, SURVEY §8(d) seeds)",
+        "config": {"workload": f"{args.workload}: " + {
+            "c1": "register 10 keys x 200 ops, 5 clients",
+            "c2": "register 1 key x 5k ops, 16 clients",
+            "c3": "jepsen.independent cas-register 1k keys x 1k ops per GPU, 5 clients/key",
+            "c4": "register 1 key x 100k ops, 16 clients, crashed :info ops",
+            "c5": "counter 1M ops, 16 clients"}[args.workload],
+            "histories_per_gpu": h.n_hist, "ops_per_gpu": ops_rank, "p_info": cfg["p_info"],
+            "scale": args.scale, "parallelism": f"keys sharded over {world} GPU(s)"},
+        "configs_explored_per_s": total_cfg / elapsed,
+        "kernel_ms_per_step": kernel_ms / args.steps,
+        "verdicts": vcount,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "lc::search_kernel", "alg_bytes_per_launch": alg_bytes,
+                     "config_bytes": st["config_bytes"], "grid_phases": st["phases"],
+                     "ret_steps": st["steps"], "candidates": st["candidates"],
+                     "spill_inserts": st["spill_inserts"]},
+        "cpu_baseline": cpu,
+        "parity_sample": parity,
+    }
+    print(json.dumps(out), flush=True)
+    plan.close()
+    if dist:
+        dist[1].destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,141 @@
+/*
+ * lincheck.h — C-ABI of the MI355X linearizability checker (liblincheck.so).
+ *
+ * Drop-in for the reference's analysis call on its hot path:
+ *   (checker/linearizable {:model (model/cas-register) :algorithm :linear})
+ *       src/jepsen/jgroups/workload/register.clj:109-111 (inside independent/checker, :106)
+ *   (checker/linearizable {:model (CounterModel. 0) :algorithm :linear})
+ *       src/jepsen/jgroups/workload/counter.clj:135-137 (SURVEY numbering; file :250-254)
+ * Both construct a jepsen.checker/Checker whose (check test history opts) runs
+ * knossos.linear/analysis [ext] and returns {:valid? ...}. A JVM caller binds these entry
+ * points through JNA; Python binds them through ctypes (lincheck/_lib.py).
+ *
+ * Conventions: plain C types only; inputs are caller-owned and read-only during the call;
+ * outputs are caller-allocated. Every entry point returns 0 on success or a negative
+ * LC_E_* code and writes a NUL-terminated message into err (when err_len > 0). Nothing is
+ * thrown or aborted across the ABI. The library is thread-safe (one mutex per device).
+ *
+ * History encoding (one op per entry, all histories concatenated, hist_off[n_hist+1]):
+ *   type  : 0 :invoke, 1 :ok, 2 :fail, 3 :info
+ *   f     : 0 :read, 1 :write, 2 :cas, 3 :add, 4 :decr, 5 :add-and-get, 6 :decr-and-get
+ *   vflags: 0 nil, 1 scalar (v0), 2 pair [v0 v1]
+ *   index : the op's :index (NULL -> position within its history)
+ * Only client ops (integer :process) may be passed; the encoder namespace drops the rest.
+ */
+#ifndef LINCHECK_H
+#define LINCHECK_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LC_ABI_VERSION 1
+
+enum lc_model { LC_MODEL_CAS_REGISTER = 1, LC_MODEL_COUNTER = 2 };
+enum lc_valid { LC_INVALID = 0, LC_VALID = 1, LC_UNKNOWN = 2 };
+enum lc_error {
+  LC_OK = 0,
+  LC_E_ARG = -1,       /* bad argument */
+  LC_E_DEVICE = -2,    /* no usable HIP device / HIP runtime error */
+  LC_E_MEMORY = -3,    /* device memory exhausted */
+  LC_E_INTERNAL = -9,  /* kernel watchdog / internal consistency failure */
+};
+/* per-history error codes reported through out_err (valid == LC_UNKNOWN) */
+enum lc_hist_error {
+  LC_H_OK = 0,
+  LC_H_MALFORMED = -4,  /* completion without invocation, double invocation, unknown :type */
+  LC_H_WIDE = -5,       /* more concurrently pending ops than the packed key holds */
+  LC_H_MODEL = -6,      /* op the model cannot step (unknown :f, wrong value shape, overflow) */
+  LC_H_CAPACITY = -7,   /* frontier/closure exceeded max_configs or device capacity */
+};
+/* flags */
+#define LC_FLAG_BOUNDS_ONLY 0x1 /* counter: run only the bounds pre-filter (sound rejection) */
+#define LC_FLAG_NO_BOUNDS 0x2   /* counter: skip the bounds pre-filter */
+
+int32_t lc_abi_version(void);
+
+/* Number of visible HIP devices (0 when none). */
+int32_t lc_device_count(void);
+
+/*
+ * Check n_hist histories against the model (knossos.linear semantics).
+ *   model_kind   : LC_MODEL_CAS_REGISTER (initial value nil; init_value ignored) or
+ *                  LC_MODEL_COUNTER (initial value init_value)
+ *   n_gpus       : devices to spread histories over (<=0: all visible); results do not
+ *                  depend on it
+ *   max_configs  : per-history cap on |frontier| + |closure| (<=0: device capacity only);
+ *                  exceeding it reports LC_UNKNOWN with LC_H_CAPACITY (Knossos gives
+ *                  :valid? :unknown when it runs out of memory [ext])
+ * Per-history outputs (n_hist entries each; any may be NULL):
+ *   out_valid       1 true / 0 false / 2 unknown
+ *   out_fail_idx    :index of the :ok completion that could not be linearized, else -1
+ *   out_fail_inv    :index of that op's invocation, else -1
+ *   out_prev_ok     :index of the last :ok completion before it, else -1
+ *   out_explored    explored_total (SURVEY §8(a) contract), configs
+ *   out_err         LC_H_* code
+ */
+int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist,
+                 const int64_t* hist_off, const int64_t* index, const int32_t* process,
+                 const int8_t* type, const int8_t* f, const int64_t* v0, const int64_t* v1,
+                 const int8_t* vflags, int32_t n_gpus, int64_t max_configs, int32_t flags,
+                 int8_t* out_valid, int64_t* out_fail_idx, int64_t* out_fail_inv,
+                 int64_t* out_prev_ok, int64_t* out_explored, int32_t* out_err,
+                 char* err, int32_t err_len);
+
+/*
+ * After lc_check reported history `hist` invalid: up to k configs of the frontier just
+ * before the failing :ok (the :configs of a Knossos failure report [ext], compare as a
+ * set). Config i: model value state[i] (register: nil when is_nil[i]), and the pending
+ * ops it has linearized, as invocation :index values, in linearized[i*64 .. i*64+n_lin[i]).
+ * The pending ops themselves (all of them) are written to pending[0..*n_pending).
+ * Valid until the next lc_check on this thread.
+ */
+int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_nil,
+                           int64_t* linearized, int32_t* n_lin, int32_t* n_out,
+                           int64_t* pending, int32_t* n_pending, char* err, int32_t err_len);
+
+/*
+ * Counter bounds pre-filter alone: a parallel prefix scan over the
+ * history that rejects any observation outside its [lo, hi] window. Sound, not complete:
+ * out_ok = 0 implies not linearizable; out_ok = 1 decides nothing.
+ * out_bad_idx = :index of the first offending completion in history order, or -1.
+ */
+int32_t lc_counter_bounds(int64_t init_value, int32_t n_hist, const int64_t* hist_off,
+                          const int64_t* index, const int32_t* process, const int8_t* type,
+                          const int8_t* f, const int64_t* v0, const int64_t* v1,
+                          const int8_t* vflags, int8_t* out_ok, int64_t* out_bad_idx,
+                          char* err, int32_t err_len);
+
+/* ---- device-resident plans (benchmarking / repeated runs on HBM-resident inputs) ---- */
+typedef struct lc_plan lc_plan;
+
+/* Encode histories on the host and upload them to device `device`. */
+int32_t lc_plan_create(int32_t device, int32_t model_kind, int64_t init_value, int32_t n_hist,
+                       const int64_t* hist_off, const int64_t* index, const int32_t* process,
+                       const int8_t* type, const int8_t* f, const int64_t* v0,
+                       const int64_t* v1, const int8_t* vflags, int64_t max_configs,
+                       lc_plan** out, char* err, int32_t err_len);
+/* Run the search on the resident plan (synchronous). */
+int32_t lc_plan_run(lc_plan* p, char* err, int32_t err_len);
+/* Copy per-history results of the last run (same meaning as lc_check's outputs). */
+int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
+                        int64_t* out_fail_inv, int64_t* out_prev_ok, int64_t* out_explored,
+                        int32_t* out_err);
+/*
+ * Statistics of the last run, written into stats[0..n) (n <= LC_STATS_N):
+ *  0 kernel_ms (HIP events around the search launches)   1 launches
+ *  2 steps (RETURN levels, batch lock-step)               3 phases (grid barriers)
+ *  4 frontier configs read                                5 candidates routed
+ *  6 frontier configs written                             7 closure configs inserted
+ *  8 config bytes (C)                                     9 algorithmic bytes
+ * 10 workgroups                                          11 spill inserts
+ */
+#define LC_STATS_N 12
+int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
+void lc_plan_destroy(lc_plan* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

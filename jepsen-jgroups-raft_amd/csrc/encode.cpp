@@ -1,0 +1,252 @@
+// encode.cpp — see encode.hpp. Product host code (independent of oracle/).
+#include "encode.hpp"
+
+#include <algorithm>
+#include <thread>
+#include <unordered_map>
+
+#include "../../include/lincheck.h"
+
+namespace lc {
+namespace {
+
+enum { T_INVOKE = 0, T_OK = 1, T_FAIL = 2, T_INFO = 3 };
+enum { F_READ = 0, F_WRITE = 1, F_CAS = 2, F_ADD = 3, F_DECR = 4, F_AAG = 5, F_DAG = 6 };
+enum { V_NIL = 0, V_SCALAR = 1, V_PAIR = 2 };
+
+struct OneOut {
+  int32_t err = 0;
+  std::string msg;
+  int32_t live_max = 0;
+  int32_t n_states = 1;
+  int64_t n_ops = 0;
+  std::vector<int64_t> state_val;
+  std::vector<uint8_t> step_slot;
+  std::vector<int64_t> step_ninv;
+  std::vector<int64_t> step_cmp_idx, step_inv_idx;
+  std::vector<uint8_t> inv_slot, inv_kind;
+  std::vector<int64_t> inv_a, inv_b, inv_index;
+};
+
+struct Op {
+  int64_t inv_pos, cmp_pos;
+  int8_t status;  // -1 pending forever, else completion type
+  int8_t f, vflags;
+  int64_t v0, v1;
+  int slot;
+};
+
+void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o) {
+  auto IDX = [&](int64_t pos) { return a.index ? a.index[pos] : pos - b; };
+  auto fail = [&](int code, const char* m) {
+    o.err = code;
+    o.msg = m;
+  };
+  // ---- pairing (knossos.history [ext])
+  std::vector<Op> ops;
+  ops.reserve((size_t)(e - b) / 2 + 1);
+  std::vector<int64_t> op_of(e - b, -1);
+  std::unordered_map<int32_t, int64_t> pend;
+  pend.reserve(64);
+  for (int64_t i = b; i < e; ++i) {
+    int8_t t = a.type[i];
+    auto it = pend.find(a.process[i]);
+    if (t == T_INVOKE) {
+      if (it != pend.end() && it->second >= 0)
+        return fail(LC_H_MALFORMED, "process invoked while an op was outstanding");
+      Op op{i, -1, -1, a.f[i], a.vflags[i], a.v0[i], a.v1[i], -1};
+      pend[a.process[i]] = (int64_t)ops.size();
+      op_of[i - b] = (int64_t)ops.size();
+      ops.push_back(op);
+      o.n_ops++;
+    } else if (t == T_OK || t == T_FAIL || t == T_INFO) {
+      if (it == pend.end() || it->second < 0)
+        return fail(LC_H_MALFORMED, "completion without an outstanding invocation");
+      Op& op = ops[it->second];
+      op.cmp_pos = i;
+      op.status = t;
+      if (t == T_OK) {  // fold the completion's value into the invocation
+        op.vflags = a.vflags[i];
+        op.v0 = a.v0[i];
+        op.v1 = a.v1[i];
+      }
+      op_of[i - b] = it->second;
+      it->second = -1;
+    } else {
+      return fail(LC_H_MALFORMED, "unknown :type");
+    }
+  }
+
+  // ---- model operands (memo for cas-register)
+  std::unordered_map<int64_t, int32_t> sid;  // value -> state id (id 0 = nil)
+  auto id_of = [&](int64_t v) -> int32_t {
+    auto it = sid.find(v);
+    if (it != sid.end()) return it->second;
+    int32_t id = (int32_t)sid.size() + 1;
+    sid.emplace(v, id);
+    o.state_val.push_back(v);
+    return id;
+  };
+  std::vector<uint8_t> kind(ops.size(), 0);
+  std::vector<int64_t> opa(ops.size(), 0), opb(ops.size(), 0);
+  if (model == LC_MODEL_CAS_REGISTER) {
+    // pass 1: values the register can hold (knossos.model/CASRegister [ext])
+    for (auto& op : ops) {
+      if (op.status == T_FAIL) continue;
+      if (op.f == F_WRITE && op.vflags == V_SCALAR) id_of(op.v0);
+      if (op.f == F_CAS && op.vflags == V_PAIR) id_of(op.v1);
+    }
+    for (size_t k = 0; k < ops.size(); ++k) {
+      const Op& op = ops[k];
+      if (op.status == T_FAIL) continue;
+      auto lookup = [&](int64_t v) -> int64_t {
+        auto it = sid.find(v);
+        return it == sid.end() ? R_NEVER : it->second;
+      };
+      switch (op.f) {
+        case F_WRITE:  // write v -> v
+          if (op.vflags == V_PAIR) return fail(LC_H_MODEL, "write with a pair value");
+          opa[k] = R_ANY;
+          opb[k] = op.vflags == V_NIL ? 0 : sid[op.v0];
+          break;
+        case F_CAS:  // cas [cur new] -> new iff cur = value
+          if (op.vflags != V_PAIR) return fail(LC_H_MODEL, "cas without [cur new]");
+          opa[k] = lookup(op.v0);
+          opb[k] = sid[op.v1];
+          break;
+        case F_READ:  // read v -> ok iff v nil or v = value
+          if (op.vflags == V_PAIR) return fail(LC_H_MODEL, "read with a pair value");
+          opa[k] = op.vflags == V_NIL ? R_ANY : lookup(op.v0);
+          opb[k] = R_KEEP;
+          break;
+        default:
+          return fail(LC_H_MODEL, "unknown :f for cas-register");
+      }
+    }
+    o.n_states = (int32_t)sid.size() + 1;
+    if (o.n_states > 65535) return fail(LC_H_WIDE, "more than 65535 distinct register values");
+  } else {
+    // CounterModel.step, counter.clj:102-127
+    for (size_t k = 0; k < ops.size(); ++k) {
+      const Op& op = ops[k];
+      if (op.status == T_FAIL) continue;
+      switch (op.f) {
+        case F_ADD:
+        case F_DECR:
+          if (op.vflags != V_SCALAR) return fail(LC_H_MODEL, ":add/:decr need a scalar delta");
+          kind[k] = op.f == F_DECR ? C_SUB : 0;
+          opb[k] = op.v0;
+          break;
+        case F_READ:
+          if (op.vflags == V_PAIR) return fail(LC_H_MODEL, ":read with a pair value");
+          kind[k] = op.vflags == V_NIL ? 0 : C_PRE_EQ;
+          opa[k] = op.v0;
+          opb[k] = 0;
+          break;
+        case F_AAG:
+        case F_DAG:
+          if (op.vflags == V_NIL) return fail(LC_H_MODEL, "*-and-get without a delta");
+          kind[k] = (op.f == F_DAG ? C_SUB : 0) | (op.vflags == V_PAIR ? C_POST_EQ : 0);
+          opb[k] = op.v0;
+          opa[k] = op.vflags == V_PAIR ? op.v1 : 0;
+          break;
+        default:
+          return fail(LC_H_MODEL, "unknown :f for CounterModel");
+      }
+    }
+  }
+
+  // ---- RETURN steps with slot assignment (lowest free slot first)
+  uint64_t used = 0;
+  int64_t ninv_cur = 0;
+  for (int64_t i = b; i < e; ++i) {
+    int64_t k = op_of[i - b];
+    if (k < 0) continue;
+    Op& op = ops[k];
+    int8_t t = a.type[i];
+    if (t == T_INVOKE) {
+      if (op.status == T_FAIL) continue;  // failed ops never enter the search
+      if (used == ~0ull >> (64 - MAX_SLOTS)) return fail(LC_H_WIDE, "more than 63 pending ops");
+      int s = __builtin_ctzll(~used);
+      used |= 1ull << s;
+      op.slot = s;
+      o.live_max = std::max(o.live_max, 64 - __builtin_clzll(used));
+      o.inv_slot.push_back((uint8_t)s);
+      o.inv_kind.push_back(kind[k]);
+      o.inv_a.push_back(opa[k]);
+      o.inv_b.push_back(opb[k]);
+      o.inv_index.push_back(IDX(op.inv_pos));
+      ninv_cur++;
+    } else if (t == T_OK) {
+      o.step_slot.push_back((uint8_t)op.slot);
+      o.step_ninv.push_back(ninv_cur);
+      o.step_cmp_idx.push_back(IDX(i));
+      o.step_inv_idx.push_back(IDX(op.inv_pos));
+      ninv_cur = 0;
+      used &= ~(1ull << op.slot);
+    }
+  }
+  // invocations after the last RETURN never matter: drop them
+  size_t keep = o.inv_slot.size() - (size_t)ninv_cur;
+  o.inv_slot.resize(keep);
+  o.inv_kind.resize(keep);
+  o.inv_a.resize(keep);
+  o.inv_b.resize(keep);
+  o.inv_index.resize(keep);
+}
+
+}  // namespace
+
+void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
+            const HistArrays& a, Encoded& out) {
+  out = Encoded();
+  out.model = model;
+  out.n_hist = n_hist;
+  out.init_value = init_value;
+  std::vector<OneOut> parts(n_hist);
+  int nt = (int)std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  if (hist_off[n_hist] < 200000) nt = 1;
+  std::vector<std::thread> th;
+  for (int w = 0; w < nt; ++w)
+    th.emplace_back([&, w] {
+      for (int h = w; h < n_hist; h += nt) encode_one(model, a, hist_off[h], hist_off[h + 1], parts[h]);
+    });
+  for (auto& t : th) t.join();
+
+  out.step_off.assign(n_hist + 1, 0);
+  out.state_off.assign(n_hist + 1, 0);
+  out.inv_off.push_back(0);
+  for (int h = 0; h < n_hist; ++h) {
+    OneOut& o = parts[h];
+    if (o.err) {  // a failed history contributes no steps
+      o.step_slot.clear();
+      o.step_ninv.clear();
+      o.inv_slot.clear();
+    }
+    out.err.push_back(o.err);
+    out.errmsg.push_back(o.msg);
+    out.live_max.push_back(o.live_max);
+    out.n_states.push_back(o.n_states);
+    out.n_ops.push_back(o.n_ops);
+    out.state_val.insert(out.state_val.end(), o.state_val.begin(), o.state_val.end());
+    out.state_off[h + 1] = (int64_t)out.state_val.size();
+    size_t inv_base = out.inv_slot.size();
+    for (size_t s = 0; s < o.step_slot.size(); ++s) {
+      out.step_slot.push_back(o.step_slot[s]);
+      out.step_cmp_idx.push_back(o.step_cmp_idx[s]);
+      out.step_inv_idx.push_back(o.step_inv_idx[s]);
+      inv_base += (size_t)o.step_ninv[s];
+      out.inv_off.push_back((int64_t)inv_base);
+    }
+    if (!o.err) {
+      out.inv_slot.insert(out.inv_slot.end(), o.inv_slot.begin(), o.inv_slot.end());
+      out.inv_kind.insert(out.inv_kind.end(), o.inv_kind.begin(), o.inv_kind.end());
+      out.inv_a.insert(out.inv_a.end(), o.inv_a.begin(), o.inv_a.end());
+      out.inv_b.insert(out.inv_b.end(), o.inv_b.begin(), o.inv_b.end());
+      out.inv_index.insert(out.inv_index.end(), o.inv_index.begin(), o.inv_index.end());
+    }
+    out.step_off[h + 1] = (int32_t)out.step_slot.size();
+  }
+}
+
+}  // namespace lc

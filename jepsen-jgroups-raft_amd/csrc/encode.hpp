@@ -1,0 +1,68 @@
+// encode.hpp — host-side history preprocessing for the GPU search (product code).
+//
+// Restates, for the device layout, what Knossos does before its search [ext]:
+//   knossos.history: pair each :invoke with the next completion of the same process;
+//     :ok folds its value into the invocation; :fail drops the pair; :info (or no
+//     completion) leaves the invocation pending forever.
+//   knossos.model.memo: map a cas-register's reachable values to dense state ids and the
+//     history's ops to transition operands (§8(a) a8; model register.clj:110).
+// and compiles the event stream into RETURN steps: step t = (slot of the returning op,
+// the invocations that happened since step t-1 with the slots they occupy). Slots are
+// reused after a return; a crashed op keeps its slot forever.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace lc {
+
+// register op operands: a = expected state id (-1 any, -2 never), b = new state id (-1 keep)
+constexpr int64_t R_ANY = -1, R_NEVER = -2, R_KEEP = -1;
+// counter op kind bits: PRE_EQ (state == a), POST_EQ (state +/- d == a), SUB (d subtracted)
+constexpr uint8_t C_PRE_EQ = 1, C_POST_EQ = 2, C_SUB = 4;
+constexpr int MAX_SLOTS = 63;
+
+struct HistArrays {
+  int64_t n;
+  const int64_t* index;  // may be null
+  const int32_t* process;
+  const int8_t* type;
+  const int8_t* f;
+  const int64_t* v0;
+  const int64_t* v1;
+  const int8_t* vflags;
+};
+
+struct Encoded {
+  int model = 0;
+  int n_hist = 0;
+  int64_t init_value = 0;
+  // per history
+  std::vector<int32_t> step_off;   // n_hist+1, into per-step arrays
+  std::vector<int32_t> err;        // LC_H_* (0 ok)
+  std::vector<std::string> errmsg;
+  std::vector<int32_t> live_max;   // max concurrently live slots
+  std::vector<int32_t> n_states;   // register: distinct states (id 0 = nil)
+  std::vector<int64_t> state_off;  // n_hist+1 into state_val (register id -> value, id>=1)
+  std::vector<int64_t> state_val;
+  std::vector<int64_t> n_ops;      // invocations (before :fail removal)
+  // per step (all histories concatenated)
+  std::vector<uint8_t> step_slot;     // slot of the returning op
+  std::vector<int64_t> inv_off;       // total_steps+1, into per-invoke arrays
+  std::vector<int64_t> step_cmp_idx;  // :index of the :ok completion
+  std::vector<int64_t> step_inv_idx;  // :index of its invocation
+  // per invoke assignment
+  std::vector<uint8_t> inv_slot;
+  std::vector<uint8_t> inv_kind;
+  std::vector<int64_t> inv_a, inv_b;
+  std::vector<int64_t> inv_index;  // :index of the invocation (failure reports)
+
+  int64_t total_steps() const { return (int64_t)step_slot.size(); }
+  int32_t n_steps(int h) const { return step_off[h + 1] - step_off[h]; }
+};
+
+// model: 1 cas-register, 2 counter. Never throws; per-history problems land in err/errmsg.
+void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
+            const HistArrays& a, Encoded& out);
+
+}  // namespace lc

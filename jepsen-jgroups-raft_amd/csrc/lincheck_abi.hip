@@ -1,0 +1,760 @@
+// lincheck_abi.hip — host side of liblincheck.so: device plans, batching, capacity growth,
+// multi-GPU key sharding and the extern "C" entry points declared in include/lincheck.h.
+//
+// Replaces, at the drop-in boundary, the call the reference makes through
+//   (checker/linearizable {:model m :algorithm :linear})   register.clj:109-111, counter.clj:135-137
+// and, for many keys at once, jepsen.independent/checker's per-key loop (register.clj:106).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <climits>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/lincheck.h"
+#include "bounds.hpp"
+#include "encode.hpp"
+#include "search.hpp"
+
+namespace lc {
+namespace {
+
+void set_err(char* err, int32_t len, const char* fmt, ...) {
+  if (!err || len <= 0) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(err, (size_t)len, fmt, ap);
+  va_end(ap);
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      last_error = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+      return e_ == hipErrorOutOfMemory ? LC_E_MEMORY : LC_E_DEVICE;                \
+    }                                                                              \
+  } while (0)
+
+std::mutex& device_mutex(int dev) {
+  static std::mutex mus[64];
+  return mus[dev & 63];
+}
+
+int bits_for(int64_t n) {  // bits to represent values 0..n-1
+  int b = 0;
+  while ((1ll << b) < n) ++b;
+  return b;
+}
+
+struct DevArray {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevArray() { release(); }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    if (n == 0) n = 8;
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) bytes = n;
+    else p = nullptr;
+    return e;
+  }
+  template <typename T>
+  T* as() const { return (T*)p; }
+};
+
+}  // namespace
+}  // namespace lc
+
+using namespace lc;
+
+struct lc_plan {
+  int device = 0;
+  int model = 0;
+  int64_t max_configs = 0;
+  Encoded enc;
+  std::string last_error;
+  // batches of histories sharing one packed key layout
+  struct Batch {
+    int h0, h1, mask_bits, state_bits, hist_bits;
+  };
+  std::vector<Batch> batches;
+  int nwg = 0, cell_cap = 256, f_cap = 16384, spill_log = 14;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // device copies of the encoded history
+  DevArray d_step_off, d_step_slot, d_inv_off, d_inv_slot, d_inv_kind, d_inv_a, d_inv_b, d_init;
+  // per-history work state (sized for the largest batch)
+  DevArray d_live, d_opk, d_opa, d_opb, d_status, d_fail, d_nonempty, d_explored;
+  // per-owner storage
+  DevArray d_flist, d_fcount, d_cells, d_cellcnt, d_spill, d_spillpos;
+  DevArray d_bar, d_produced, d_running, d_flags, d_stats;
+  bool spill_clean = false;
+  // results
+  std::vector<int32_t> status, fail_step;
+  std::vector<unsigned long long> explored;
+  double stats[LC_STATS_N] = {0};
+  int32_t max_t = INT32_MAX;  // failure-frontier dump mode
+  int64_t entry_bytes() const { return model == LC_MODEL_CAS_REGISTER ? 8 : 16; }
+
+  ~lc_plan() {
+    if (ev0) hipEventDestroy(ev0);
+    if (ev1) hipEventDestroy(ev1);
+    if (stream) hipStreamDestroy(stream);
+  }
+
+  void make_batches() {
+    batches.clear();
+    const int n = enc.n_hist;
+    for (int h = 0; h < n; ++h) {  // a key must hold [state | mask] of one history in 63 bits
+      const int sb = model == LC_MODEL_CAS_REGISTER ? bits_for(enc.n_states[h]) : 0;
+      if (!enc.err[h] && enc.live_max[h] + sb > 63) {
+        enc.err[h] = LC_H_WIDE;
+        enc.errmsg[h] = "pending ops + state bits exceed the 63-bit packed config";
+      }
+    }
+    int h = 0;
+    while (h < n) {
+      Batch b{h, h, 1, 0, 0};
+      int mb = 1, sb = 0;
+      int e = h;
+      while (e < n && e - h < HMAX) {
+        int mb2 = std::max(mb, enc.live_max[e]);
+        int sb2 = model == LC_MODEL_CAS_REGISTER ? std::max(sb, bits_for(enc.n_states[e])) : 0;
+        int hb2 = bits_for(e - h + 1);
+        if (mb2 + sb2 + hb2 > 63) break;
+        mb = mb2;
+        sb = sb2;
+        ++e;
+      }
+      if (e == h) e = h + 1;  // a single history always forms a batch (encoder bounds it)
+      b.h1 = e;
+      b.mask_bits = mb;
+      b.state_bits = sb;
+      b.hist_bits = bits_for(e - h);
+      batches.push_back(b);
+      h = e;
+    }
+  }
+
+  template <typename T>
+  int upload(DevArray& d, const std::vector<T>& v) {
+    HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1) * sizeof(T)));
+    if (!v.empty()) HIP_TRY(hipMemcpy(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return 0;
+  }
+
+  int init_device() {
+    HIP_TRY(hipSetDevice(device));
+    if (!stream) HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    if (!ev0) HIP_TRY(hipEventCreate(&ev0));
+    if (!ev1) HIP_TRY(hipEventCreate(&ev1));
+    nwg = search_grid_size(model);
+    if (nwg <= 0) {
+      last_error = "search kernel cannot be resident (occupancy 0)";
+      return LC_E_DEVICE;
+    }
+    return 0;
+  }
+
+  int upload_encoded() {
+    std::vector<int64_t> init(enc.n_hist);
+    for (int h = 0; h < enc.n_hist; ++h) init[h] = model == LC_MODEL_CAS_REGISTER ? 0 : enc.init_value;
+    int rc;
+    if ((rc = upload(d_step_off, enc.step_off))) return rc;
+    if ((rc = upload(d_step_slot, enc.step_slot))) return rc;
+    if ((rc = upload(d_inv_off, enc.inv_off))) return rc;
+    if ((rc = upload(d_inv_slot, enc.inv_slot))) return rc;
+    if ((rc = upload(d_inv_kind, enc.inv_kind))) return rc;
+    if ((rc = upload(d_inv_a, enc.inv_a))) return rc;
+    if ((rc = upload(d_inv_b, enc.inv_b))) return rc;
+    if ((rc = upload(d_init, init))) return rc;
+    return 0;
+  }
+
+  int ensure_work(int nh) {
+    HIP_TRY(d_live.ensure(2ull * nh * 8));
+    HIP_TRY(d_opk.ensure(2ull * nh * 64));
+    HIP_TRY(d_opa.ensure(2ull * nh * 64 * 8));
+    HIP_TRY(d_opb.ensure(2ull * nh * 64 * 8));
+    HIP_TRY(d_status.ensure((size_t)nh * 4));
+    HIP_TRY(d_fail.ensure((size_t)nh * 4));
+    HIP_TRY(d_nonempty.ensure(2ull * nh * 4));
+    HIP_TRY(d_explored.ensure((size_t)nh * 8));
+    const size_t E = (size_t)entry_bytes();
+    HIP_TRY(d_flist.ensure(2ull * nwg * f_cap * E));
+    HIP_TRY(d_fcount.ensure(2ull * nwg * 4));
+    HIP_TRY(d_cells.ensure(2ull * nwg * nwg * cell_cap * E));
+    HIP_TRY(d_cellcnt.ensure(2ull * nwg * nwg * 4));
+    size_t sp = (size_t)nwg << spill_log;
+    if (d_spill.bytes < sp * 8) {
+      HIP_TRY(d_spill.ensure(sp * 8));
+      spill_clean = false;
+    }
+    HIP_TRY(d_spillpos.ensure(sp * 4));
+    HIP_TRY(d_bar.ensure(sizeof(GridBar)));
+    HIP_TRY(d_produced.ensure(4 * 8));
+    HIP_TRY(d_running.ensure(4 * 4));
+    HIP_TRY(d_flags.ensure(FL_N * 4));
+    HIP_TRY(d_stats.ensure(SS_N * 8));
+    return 0;
+  }
+
+  // run one batch; returns 0, LC_E_* on hard errors, 1 when capacities must grow
+  int run_batch(const Batch& bt, float* ms) {
+    const int nh = bt.h1 - bt.h0;
+    int rc = ensure_work(nh);
+    if (rc) return rc;
+    std::vector<int32_t> st0(nh);
+    for (int i = 0; i < nh; ++i) st0[i] = enc.err[bt.h0 + i] ? ST_SKIP : ST_RUNNING;
+    HIP_TRY(hipMemcpyAsync(d_status.p, st0.data(), nh * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemsetAsync(d_live.p, 0, 2ull * nh * 8, stream));
+    HIP_TRY(hipMemsetAsync(d_fail.p, 0xff, (size_t)nh * 4, stream));
+    HIP_TRY(hipMemsetAsync(d_nonempty.p, 0, 2ull * nh * 4, stream));
+    HIP_TRY(hipMemsetAsync(d_explored.p, 0, (size_t)nh * 8, stream));
+    if (!spill_clean) {
+      HIP_TRY(hipMemsetAsync(d_spill.p, 0xff, ((size_t)nwg << spill_log) * 8, stream));
+      spill_clean = true;
+    }
+    HIP_TRY(hipMemsetAsync(d_bar.p, 0, sizeof(GridBar), stream));
+    HIP_TRY(hipMemsetAsync(d_produced.p, 0, 32, stream));
+    HIP_TRY(hipMemsetAsync(d_running.p, 0, 16, stream));
+    HIP_TRY(hipMemsetAsync(d_flags.p, 0, FL_N * 4, stream));
+    HIP_TRY(hipMemsetAsync(d_stats.p, 0, SS_N * 8, stream));
+
+    SearchParams p{};
+    p.n_hist = nh;
+    p.nwg = nwg;
+    p.mask_bits = bt.mask_bits;
+    p.state_shift = bt.mask_bits;
+    p.hist_shift = bt.mask_bits + bt.state_bits;
+    p.cell_cap = cell_cap;
+    p.f_cap = f_cap;
+    p.spill_log = spill_log;
+    p.max_t = max_t;
+    p.model = model;
+    p.step_off = d_step_off.as<int32_t>() + bt.h0;
+    p.step_slot = d_step_slot.as<uint8_t>();
+    p.inv_off = d_inv_off.as<int64_t>();
+    p.inv_slot = d_inv_slot.as<uint8_t>();
+    p.inv_kind = d_inv_kind.as<uint8_t>();
+    p.inv_a = d_inv_a.as<int64_t>();
+    p.inv_b = d_inv_b.as<int64_t>();
+    p.init_st = d_init.as<int64_t>() + bt.h0;
+    p.live = d_live.as<uint64_t>();
+    p.op_kind = d_opk.as<uint8_t>();
+    p.op_a = d_opa.as<int64_t>();
+    p.op_b = d_opb.as<int64_t>();
+    p.status = d_status.as<int32_t>();
+    p.fail_step = d_fail.as<int32_t>();
+    p.nonempty = d_nonempty.as<uint32_t>();
+    p.explored = d_explored.as<unsigned long long>();
+    p.flist = d_flist.p;
+    p.fcount = d_fcount.as<uint32_t>();
+    p.cells = d_cells.p;
+    p.cell_cnt = d_cellcnt.as<uint32_t>();
+    p.spill = d_spill.as<uint64_t>();
+    p.spill_pos = d_spillpos.as<uint32_t>();
+    p.bar = d_bar.as<GridBar>();
+    p.produced = d_produced.as<unsigned long long>();
+    p.running = d_running.as<unsigned>();
+    p.flags = d_flags.as<int32_t>();
+    p.stats = d_stats.as<unsigned long long>();
+
+    HIP_TRY(hipEventRecord(ev0, stream));
+    HIP_TRY(launch_search(p, stream));
+    HIP_TRY(hipEventRecord(ev1, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
+    *ms += t;
+
+    int32_t flags[FL_N];
+    HIP_TRY(hipMemcpy(flags, d_flags.p, sizeof(flags), hipMemcpyDeviceToHost));
+    if (flags[FL_ABORT]) {
+      last_error = "search kernel watchdog: grid barrier timed out";
+      return LC_E_INTERNAL;
+    }
+    if (flags[FL_SPILL]) {
+      spill_clean = false;  // a full spill table may hold stale entries
+      return 1 + 1;
+    }
+    if (flags[FL_OVERFLOW]) return 1;
+
+    std::vector<int32_t> st(nh), fs(nh);
+    std::vector<unsigned long long> ex(nh);
+    HIP_TRY(hipMemcpy(st.data(), d_status.p, nh * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fs.data(), d_fail.p, nh * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(ex.data(), d_explored.p, nh * 8, hipMemcpyDeviceToHost));
+    unsigned long long ss[SS_N];
+    HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
+    for (int i = 0; i < nh; ++i) {
+      status[bt.h0 + i] = st[i];
+      fail_step[bt.h0 + i] = fs[i];
+      explored[bt.h0 + i] = ex[i];
+    }
+    stats[1] += 1;
+    stats[2] += (double)ss[SS_STEPS];
+    stats[3] += (double)ss[SS_PHASES];
+    stats[4] += (double)ss[SS_FIN];
+    stats[5] += (double)ss[SS_CAND];
+    stats[6] += (double)ss[SS_FOUT];
+    stats[7] += (double)ss[SS_SNEW];
+    stats[11] += (double)ss[SS_SPILL];
+    return 0;
+  }
+
+  size_t device_budget() {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
+    return free_b;
+  }
+
+  int run() {
+    int rc;
+    HIP_TRY(hipSetDevice(device));
+    status.assign(enc.n_hist, ST_SKIP);
+    fail_step.assign(enc.n_hist, -1);
+    explored.assign(enc.n_hist, 0);
+    std::fill(stats, stats + LC_STATS_N, 0.0);
+    float ms = 0;
+    for (size_t bi = 0; bi < batches.size(); ++bi) {
+      const Batch& bt = batches[bi];
+      for (int attempt = 0;; ++attempt) {
+        rc = run_batch(bt, &ms);
+        if (rc <= 0) break;
+        // grow what overflowed, bounded by max_configs and free HBM
+        const size_t E = (size_t)entry_bytes();
+        size_t need = 0;
+        if (rc == 2) {
+          spill_log += 2;
+          need = ((size_t)nwg << spill_log) * 12;
+        } else {
+          cell_cap *= 4;
+          f_cap *= 4;
+          need = 2ull * nwg * nwg * cell_cap * E + 2ull * nwg * f_cap * E;
+        }
+        bool over_cfg = max_configs > 0 && (int64_t)nwg * f_cap > 4 * max_configs;
+        if (over_cfg || need > device_budget() * 9 / 10 || attempt > 6 || spill_log > 24) {
+          // capacity exhausted: the batch's histories are undecided (Knossos: :unknown)
+          for (int h = bt.h0; h < bt.h1; ++h) status[h] = enc.err[h] ? ST_SKIP : ST_CAPACITY;
+          rc = 0;
+          break;
+        }
+        d_cells.release();
+        d_flist.release();
+      }
+      if (rc < 0) return rc;
+    }
+    stats[0] = ms;
+    stats[7] = 0;
+    for (auto x : explored) stats[7] += (double)x;
+    stats[8] = (double)entry_bytes();
+    // bytes_alg = F_in*C + N_cand*(C+8) + F_out*C
+    const double C = stats[8];
+    stats[9] = stats[4] * C + stats[5] * (C + 8) + stats[6] * C;
+    stats[10] = nwg;
+    return 0;
+  }
+
+  void results(int8_t* v, int64_t* fi, int64_t* finv, int64_t* pok, int64_t* ex,
+               int32_t* er) const {
+    for (int h = 0; h < enc.n_hist; ++h) {
+      int8_t valid = LC_UNKNOWN;
+      int32_t code = enc.err[h];
+      int64_t a = -1, b = -1, c = -1;
+      switch (status[h]) {
+        case ST_VALID: valid = LC_VALID; break;
+        case ST_INVALID: {
+          valid = LC_INVALID;
+          const int64_t g = (int64_t)enc.step_off[h] + fail_step[h];
+          a = enc.step_cmp_idx[g];
+          b = enc.step_inv_idx[g];
+          c = fail_step[h] > 0 ? enc.step_cmp_idx[g - 1] : -1;
+          break;
+        }
+        case ST_CAPACITY: code = LC_H_CAPACITY; break;
+        case ST_MODEL: code = LC_H_MODEL; break;
+        default: break;
+      }
+      if (v) v[h] = valid;
+      if (fi) fi[h] = a;
+      if (finv) finv[h] = b;
+      if (pok) pok[h] = c;
+      if (ex) ex[h] = (int64_t)explored[h];
+      if (er) er[h] = code;
+    }
+  }
+};
+
+namespace {
+
+int plan_build(int device, int model, int64_t init_value, int n_hist, const int64_t* hist_off,
+               const HistArrays& a, int64_t max_configs, lc_plan** out, std::string& msg) {
+  auto p = std::make_unique<lc_plan>();
+  p->device = device;
+  p->model = model;
+  p->max_configs = max_configs;
+  encode(model, init_value, n_hist, hist_off, a, p->enc);
+  p->make_batches();
+  int rc = p->init_device();
+  if (!rc) rc = p->upload_encoded();
+  if (rc) {
+    msg = p->last_error;
+    return rc;
+  }
+  *out = p.release();
+  return 0;
+}
+
+bool valid_args(int model, int n_hist, const int64_t* hist_off, const int32_t* process,
+                const int8_t* type, const int8_t* f, const int64_t* v0, const int64_t* v1,
+                const int8_t* vflags, char* err, int32_t err_len) {
+  if (model != LC_MODEL_CAS_REGISTER && model != LC_MODEL_COUNTER) {
+    set_err(err, err_len, "unknown model kind %d", model);
+    return false;
+  }
+  if (n_hist < 0 || !hist_off) {
+    set_err(err, err_len, "n_hist < 0 or hist_off NULL");
+    return false;
+  }
+  for (int h = 0; h < n_hist; ++h)
+    if (hist_off[h + 1] < hist_off[h]) {
+      set_err(err, err_len, "hist_off not monotone at %d", h);
+      return false;
+    }
+  if (hist_off[n_hist] > hist_off[0] && (!process || !type || !f || !v0 || !v1 || !vflags)) {
+    set_err(err, err_len, "NULL history array");
+    return false;
+  }
+  return true;
+}
+
+// state of the most recent lc_check on this thread (for lc_failure_configs)
+struct LastCheck {
+  int model = 0, device = 0;
+  int64_t init_value = 0;
+  std::vector<int64_t> off, index, v0, v1;
+  std::vector<int32_t> process;
+  std::vector<int8_t> type, f, vflags;
+  std::vector<int8_t> valid;
+  bool have = false;
+};
+thread_local LastCheck g_last;
+
+}  // namespace
+
+extern "C" {
+
+int32_t lc_abi_version(void) { return LC_ABI_VERSION; }
+
+int32_t lc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int32_t lc_plan_create(int32_t device, int32_t model_kind, int64_t init_value, int32_t n_hist,
+                       const int64_t* hist_off, const int64_t* index, const int32_t* process,
+                       const int8_t* type, const int8_t* f, const int64_t* v0, const int64_t* v1,
+                       const int8_t* vflags, int64_t max_configs, lc_plan** out, char* err,
+                       int32_t err_len) {
+  if (!out) return LC_E_ARG;
+  *out = nullptr;
+  if (!valid_args(model_kind, n_hist, hist_off, process, type, f, v0, v1, vflags, err, err_len))
+    return LC_E_ARG;
+  if (lc_device_count() <= device || device < 0) {
+    set_err(err, err_len, "no HIP device %d (the checker has no CPU fallback)", device);
+    return LC_E_DEVICE;
+  }
+  std::lock_guard<std::mutex> g(device_mutex(device));
+  HistArrays a{hist_off[n_hist] - hist_off[0], index, process, type, f, v0, v1, vflags};
+  std::string msg;
+  int rc = plan_build(device, model_kind, init_value, n_hist, hist_off, a, max_configs, out, msg);
+  if (rc) set_err(err, err_len, "%s", msg.c_str());
+  return rc;
+}
+
+int32_t lc_plan_run(lc_plan* p, char* err, int32_t err_len) {
+  if (!p) return LC_E_ARG;
+  std::lock_guard<std::mutex> g(device_mutex(p->device));
+  int rc = p->run();
+  if (rc) set_err(err, err_len, "%s", p->last_error.c_str());
+  return rc;
+}
+
+int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx, int64_t* out_fail_inv,
+                        int64_t* out_prev_ok, int64_t* out_explored, int32_t* out_err) {
+  if (!p) return LC_E_ARG;
+  p->results(out_valid, out_fail_idx, out_fail_inv, out_prev_ok, out_explored, out_err);
+  return 0;
+}
+
+int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n) {
+  if (!p || !stats) return LC_E_ARG;
+  for (int i = 0; i < n && i < LC_STATS_N; ++i) stats[i] = p->stats[i];
+  return 0;
+}
+
+void lc_plan_destroy(lc_plan* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> g(device_mutex(p->device));
+  hipSetDevice(p->device);
+  delete p;
+}
+
+int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const int64_t* hist_off,
+                 const int64_t* index, const int32_t* process, const int8_t* type, const int8_t* f,
+                 const int64_t* v0, const int64_t* v1, const int8_t* vflags, int32_t n_gpus,
+                 int64_t max_configs, int32_t flags, int8_t* out_valid, int64_t* out_fail_idx,
+                 int64_t* out_fail_inv, int64_t* out_prev_ok, int64_t* out_explored,
+                 int32_t* out_err, char* err, int32_t err_len) {
+  if (!valid_args(model_kind, n_hist, hist_off, process, type, f, v0, v1, vflags, err, err_len))
+    return LC_E_ARG;
+  const int ndev = lc_device_count();
+  if (ndev <= 0) {
+    set_err(err, err_len, "no HIP device visible (the checker has no CPU fallback)");
+    return LC_E_DEVICE;
+  }
+  int G = n_gpus <= 0 ? ndev : std::min(n_gpus, ndev);
+  G = std::max(1, std::min(G, std::max(1, n_hist)));
+
+  // keep a copy for lc_failure_configs
+  g_last = LastCheck();
+  g_last.model = model_kind;
+  g_last.init_value = init_value;
+  {
+    const int64_t n = hist_off[n_hist] - hist_off[0], b = hist_off[0];
+    g_last.off.assign(hist_off, hist_off + n_hist + 1);
+    for (auto& x : g_last.off) x -= b;
+    auto cp = [&](auto& dst, const auto* src) {
+      if (src) dst.assign(src + b, src + b + n);
+    };
+    cp(g_last.index, index);
+    cp(g_last.process, process);
+    cp(g_last.type, type);
+    cp(g_last.f, f);
+    cp(g_last.v0, v0);
+    cp(g_last.v1, v1);
+    cp(g_last.vflags, vflags);
+    if (!index) {  // :index defaults to the position within each history
+      g_last.index.resize(n);
+      for (int h = 0; h < n_hist; ++h)
+        for (int64_t i = g_last.off[h]; i < g_last.off[h + 1]; ++i) g_last.index[i] = i - g_last.off[h];
+    }
+  }
+  const LastCheck& L = g_last;
+
+  // bounds pre-filter for counters (sound rejection only; never changes a verdict's index)
+  std::vector<int8_t> bounds_ok(n_hist, 1);
+  std::vector<int64_t> bounds_bad(n_hist, -1);
+  if (model_kind == LC_MODEL_COUNTER && (flags & LC_FLAG_BOUNDS_ONLY)) {
+    int rc = lc_counter_bounds(init_value, n_hist, L.off.data(), L.index.data(), L.process.data(),
+                               L.type.data(), L.f.data(), L.v0.data(), L.v1.data(), L.vflags.data(),
+                               bounds_ok.data(), bounds_bad.data(), err, err_len);
+    if (rc) return rc;
+    for (int h = 0; h < n_hist; ++h) {
+      if (out_valid) out_valid[h] = bounds_ok[h] ? LC_UNKNOWN : LC_INVALID;
+      if (out_fail_idx) out_fail_idx[h] = bounds_bad[h];
+      if (out_fail_inv) out_fail_inv[h] = -1;
+      if (out_prev_ok) out_prev_ok[h] = -1;
+      if (out_explored) out_explored[h] = 0;
+      if (out_err) out_err[h] = 0;
+    }
+    return 0;
+  }
+
+  // shard histories over devices: longest-processing-time on entry counts
+  std::vector<std::vector<int>> shard(G);
+  {
+    std::vector<int> order(n_hist);
+    for (int h = 0; h < n_hist; ++h) order[h] = h;
+    std::sort(order.begin(), order.end(), [&](int x, int y) {
+      return L.off[x + 1] - L.off[x] > L.off[y + 1] - L.off[y];
+    });
+    std::vector<int64_t> load(G, 0);
+    for (int h : order) {
+      int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      shard[g].push_back(h);
+      load[g] += L.off[h + 1] - L.off[h];
+    }
+    for (auto& s : shard) std::sort(s.begin(), s.end());
+  }
+  std::vector<int> rcs(G, 0);
+  std::vector<std::string> msgs(G);
+  auto work = [&](int g) {
+    const std::vector<int>& hs = shard[g];
+    if (hs.empty()) return;
+    // gather this shard's histories into contiguous arrays
+    std::vector<int64_t> off(1, 0), idx, a0, a1;
+    std::vector<int32_t> pr;
+    std::vector<int8_t> ty, ff, vf;
+    for (int h : hs) {
+      for (int64_t i = L.off[h]; i < L.off[h + 1]; ++i) {
+        idx.push_back(L.index[i]);
+        pr.push_back(L.process[i]);
+        ty.push_back(L.type[i]);
+        ff.push_back(L.f[i]);
+        a0.push_back(L.v0[i]);
+        a1.push_back(L.v1[i]);
+        vf.push_back(L.vflags[i]);
+      }
+      off.push_back((int64_t)idx.size());
+    }
+    std::lock_guard<std::mutex> lk(device_mutex(g));
+    HistArrays a{off.back(), idx.data(), pr.data(), ty.data(), ff.data(), a0.data(), a1.data(), vf.data()};
+    lc_plan* p = nullptr;
+    int rc = plan_build(g, model_kind, init_value, (int)hs.size(), off.data(), a, max_configs, &p, msgs[g]);
+    if (!rc) {
+      rc = p->run();
+      if (rc) msgs[g] = p->last_error;
+    }
+    if (!rc) {
+      const size_t m = hs.size();
+      std::vector<int8_t> v(m);
+      std::vector<int64_t> fi(m), fv(m), po(m), ex(m);
+      std::vector<int32_t> er(m);
+      p->results(v.data(), fi.data(), fv.data(), po.data(), ex.data(), er.data());
+      for (size_t k = 0; k < m; ++k) {
+        const int h = hs[k];
+        if (out_valid) out_valid[h] = v[k];
+        if (out_fail_idx) out_fail_idx[h] = fi[k];
+        if (out_fail_inv) out_fail_inv[h] = fv[k];
+        if (out_prev_ok) out_prev_ok[h] = po[k];
+        if (out_explored) out_explored[h] = ex[k];
+        if (out_err) out_err[h] = er[k];
+        g_last.valid.resize(n_hist);
+      }
+    }
+    if (p) {
+      hipSetDevice(g);
+      delete p;
+    }
+    rcs[g] = rc;
+  };
+  if (G == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; ++g) th.emplace_back(work, g);
+    for (auto& t : th) t.join();
+  }
+  for (int g = 0; g < G; ++g)
+    if (rcs[g]) {
+      set_err(err, err_len, "device %d: %s", g, msgs[g].c_str());
+      return rcs[g];
+    }
+  g_last.have = true;
+  return 0;
+}
+
+int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_nil,
+                           int64_t* linearized, int32_t* n_lin, int32_t* n_out, int64_t* pending,
+                           int32_t* n_pending, char* err, int32_t err_len) {
+  const LastCheck& L = g_last;
+  if (!L.have || hist < 0 || hist + 1 >= (int)L.off.size()) {
+    set_err(err, err_len, "no checked history %d on this thread", hist);
+    return LC_E_ARG;
+  }
+  const int64_t b = L.off[hist], e = L.off[hist + 1];
+  int64_t off[2] = {0, e - b};
+  HistArrays a{e - b, L.index.data() + b, L.process.data() + b, L.type.data() + b, L.f.data() + b,
+               L.v0.data() + b, L.v1.data() + b, L.vflags.data() + b};
+  std::lock_guard<std::mutex> lk(device_mutex(0));
+  lc_plan* p = nullptr;
+  std::string msg;
+  int rc = plan_build(0, L.model, L.init_value, 1, off, a, 0, &p, msg);
+  if (rc) {
+    set_err(err, err_len, "%s", msg.c_str());
+    return rc;
+  }
+  std::unique_ptr<lc_plan> hold(p);
+  rc = p->run();  // find the failing step
+  if (rc) {
+    set_err(err, err_len, "%s", p->last_error.c_str());
+    return rc;
+  }
+  if (p->status[0] != ST_INVALID) {
+    set_err(err, err_len, "history %d is not invalid", hist);
+    return LC_E_ARG;
+  }
+  const int t_fail = p->fail_step[0];
+  p->max_t = t_fail;  // stop before the failing RETURN: the frontier it saw stays in flist
+  rc = p->run();
+  if (rc) {
+    set_err(err, err_len, "%s", p->last_error.c_str());
+    return rc;
+  }
+  // replay slot assignments to step t_fail
+  const Encoded& en = p->enc;
+  int64_t slot_inv[64];
+  for (int s = 0; s < 64; ++s) slot_inv[s] = -1;
+  for (int t = 0; t <= t_fail; ++t) {
+    const int64_t g = en.step_off[0] + t;
+    if (t > 0) slot_inv[en.step_slot[g - 1]] = -1;
+    for (int64_t q = en.inv_off[g]; q < en.inv_off[g + 1]; ++q) slot_inv[en.inv_slot[q]] = en.inv_index[q];
+  }
+  int np = 0;
+  for (int s = 0; s < 64; ++s)
+    if (slot_inv[s] >= 0) {
+      if (pending) pending[np] = slot_inv[s];
+      ++np;
+    }
+  if (n_pending) *n_pending = np;
+  // read the frontier lists of buffer (t_fail & 1)
+  const lc_plan::Batch& bt = p->batches[0];
+  const int par = t_fail & 1;
+  std::vector<uint32_t> fc(2 * p->nwg);
+  hipMemcpy(fc.data(), p->d_fcount.p, fc.size() * 4, hipMemcpyDeviceToHost);
+  const size_t E = (size_t)p->entry_bytes();
+  std::vector<uint8_t> buf((size_t)p->f_cap * E);
+  int out = 0;
+  for (int w = 0; w < p->nwg && out < k; ++w) {
+    const uint32_t n = std::min<uint32_t>(fc[(size_t)par * p->nwg + w], (uint32_t)p->f_cap);
+    if (!n) continue;
+    hipMemcpy(buf.data(), (char*)p->d_flist.p + ((size_t)par * p->nwg + w) * p->f_cap * E, n * E,
+              hipMemcpyDeviceToHost);
+    for (uint32_t i = 0; i < n && out < k; ++i) {
+      uint64_t key;
+      memcpy(&key, buf.data() + i * E, 8);
+      int64_t val = 0;
+      int8_t nil = 0;
+      if (L.model == LC_MODEL_CAS_REGISTER) {
+        const uint64_t sm = (1ull << bt.state_bits) - 1;
+        const int64_t id = (int64_t)((key >> bt.mask_bits) & sm);
+        if (id == 0) nil = 1;
+        else val = en.state_val[en.state_off[0] + id - 1];
+      } else {
+        memcpy(&val, buf.data() + i * E + 8, 8);
+      }
+      int nl = 0;
+      for (int s = 0; s < bt.mask_bits; ++s)
+        if ((key >> s) & 1) {
+          if (linearized) linearized[(size_t)out * 64 + nl] = slot_inv[s];
+          ++nl;
+        }
+      if (state) state[out] = val;
+      if (is_nil) is_nil[out] = nil;
+      if (n_lin) n_lin[out] = nl;
+      ++out;
+    }
+  }
+  if (n_out) *n_out = out;
+  return 0;
+}
+
+}  // extern "C"

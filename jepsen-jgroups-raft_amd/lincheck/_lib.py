@@ -1,0 +1,174 @@
+"""ctypes binding of liblincheck.so — the same C-ABI a JVM caller binds through JNA
+(include/lincheck.h; INTEGRATION.md shows the JNA interface). There is deliberately no
+CPU fallback: if the library or a HIP device is missing, calls raise."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblincheck.so")
+
+# every symbol include/lincheck.h declares (tests check the exports)
+EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_failure_configs",
+           "lc_counter_bounds", "lc_plan_create", "lc_plan_run", "lc_plan_results",
+           "lc_plan_stats", "lc_plan_destroy")
+STATS_N = 12
+STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
+               "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
+               "spill_inserts")
+
+P = C.c_void_p
+I8P = C.POINTER(C.c_int8)
+_lib = None
+
+
+class LincheckError(RuntimeError):
+    pass
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LincheckError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; "
+                            "g.build()'` (the checker has no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    L.lc_abi_version.restype = C.c_int32
+    L.lc_device_count.restype = C.c_int32
+    L.lc_check.argtypes = [C.c_int32, C.c_int64, C.c_int32] + [P] * 8 + \
+        [C.c_int32, C.c_int64, C.c_int32] + [P] * 6 + [C.c_char_p, C.c_int32]
+    L.lc_check.restype = C.c_int32
+    L.lc_failure_configs.argtypes = [C.c_int32, C.c_int32] + [P] * 7 + [C.c_char_p, C.c_int32]
+    L.lc_failure_configs.restype = C.c_int32
+    L.lc_counter_bounds.argtypes = [C.c_int64, C.c_int32] + [P] * 10 + [C.c_char_p, C.c_int32]
+    L.lc_counter_bounds.restype = C.c_int32
+    L.lc_plan_create.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.c_int32] + [P] * 8 + \
+        [C.c_int64, C.POINTER(C.c_void_p), C.c_char_p, C.c_int32]
+    L.lc_plan_create.restype = C.c_int32
+    L.lc_plan_run.argtypes = [P, C.c_char_p, C.c_int32]
+    L.lc_plan_run.restype = C.c_int32
+    L.lc_plan_results.argtypes = [P] * 7
+    L.lc_plan_results.restype = C.c_int32
+    L.lc_plan_stats.argtypes = [P, P, C.c_int32]
+    L.lc_plan_stats.restype = C.c_int32
+    L.lc_plan_destroy.argtypes = [P]
+    L.lc_plan_destroy.restype = None
+    if L.lc_abi_version() != 1:
+        raise LincheckError("ABI version mismatch")
+    _lib = L
+    return L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _errbuf():
+    return C.create_string_buffer(512)
+
+
+def _raise(rc, buf, what):
+    if rc != 0:
+        raise LincheckError(f"{what} failed ({rc}): {buf.value.decode(errors='replace')}")
+
+
+MODEL_KIND = {"cas-register": 1, "counter": 2}
+
+
+def check(model_kind: int, init_value: int, h, n_gpus: int = 1, max_configs: int = 0,
+          flags: int = 0):
+    """Run lc_check on a lincheck.history.History. Returns a dict of numpy arrays."""
+    L = load()
+    n = h.n_hist
+    out = {"valid": np.zeros(n, np.int8), "fail_idx": np.zeros(n, np.int64),
+           "fail_inv": np.zeros(n, np.int64), "prev_ok": np.zeros(n, np.int64),
+           "explored": np.zeros(n, np.int64), "err": np.zeros(n, np.int32)}
+    buf = _errbuf()
+    rc = L.lc_check(model_kind, init_value, n, _p(h.off), _p(h.index), _p(h.process), _p(h.type),
+                    _p(h.f), _p(h.v0), _p(h.v1), _p(h.vflags), n_gpus, max_configs, flags,
+                    _p(out["valid"]), _p(out["fail_idx"]), _p(out["fail_inv"]), _p(out["prev_ok"]),
+                    _p(out["explored"]), _p(out["err"]), buf, len(buf))
+    _raise(rc, buf, "lc_check")
+    return out
+
+
+def failure_configs(hist: int, k: int = 10):
+    """Pre-failure frontier of history `hist` of the last check() on this thread."""
+    L = load()
+    st = np.zeros(k, np.int64)
+    nil = np.zeros(k, np.int8)
+    lin = np.zeros(k * 64, np.int64)
+    nlin = np.zeros(k, np.int32)
+    nout = np.zeros(1, np.int32)
+    pend = np.zeros(64, np.int64)
+    npend = np.zeros(1, np.int32)
+    buf = _errbuf()
+    rc = L.lc_failure_configs(hist, k, _p(st), _p(nil), _p(lin), _p(nlin), _p(nout), _p(pend),
+                              _p(npend), buf, len(buf))
+    _raise(rc, buf, "lc_failure_configs")
+    cfgs = []
+    for i in range(int(nout[0])):
+        cfgs.append((None if nil[i] else int(st[i]),
+                     tuple(sorted(int(x) for x in lin[i * 64:i * 64 + nlin[i]]))))
+    return cfgs, [int(x) for x in pend[:npend[0]]]
+
+
+def counter_bounds(init_value: int, h):
+    L = load()
+    ok = np.zeros(h.n_hist, np.int8)
+    bad = np.zeros(h.n_hist, np.int64)
+    buf = _errbuf()
+    rc = L.lc_counter_bounds(init_value, h.n_hist, _p(h.off), _p(h.index), _p(h.process),
+                             _p(h.type), _p(h.f), _p(h.v0), _p(h.v1), _p(h.vflags), _p(ok),
+                             _p(bad), buf, len(buf))
+    _raise(rc, buf, "lc_counter_bounds")
+    return ok, bad
+
+
+class Plan:
+    """Device-resident encoded histories (lc_plan_*): run() times only the search."""
+
+    def __init__(self, model_kind: int, init_value: int, h, device: int = 0, max_configs: int = 0):
+        L = load()
+        self._L = L
+        self.n_hist = h.n_hist
+        handle = C.c_void_p()
+        buf = _errbuf()
+        rc = L.lc_plan_create(device, model_kind, init_value, h.n_hist, _p(h.off), _p(h.index),
+                              _p(h.process), _p(h.type), _p(h.f), _p(h.v0), _p(h.v1),
+                              _p(h.vflags), max_configs, C.byref(handle), buf, len(buf))
+        _raise(rc, buf, "lc_plan_create")
+        self._h = handle
+
+    def run(self):
+        buf = _errbuf()
+        _raise(self._L.lc_plan_run(self._h, buf, len(buf)), buf, "lc_plan_run")
+
+    def results(self):
+        n = self.n_hist
+        out = {"valid": np.zeros(n, np.int8), "fail_idx": np.zeros(n, np.int64),
+               "fail_inv": np.zeros(n, np.int64), "prev_ok": np.zeros(n, np.int64),
+               "explored": np.zeros(n, np.int64), "err": np.zeros(n, np.int32)}
+        self._L.lc_plan_results(self._h, _p(out["valid"]), _p(out["fail_idx"]), _p(out["fail_inv"]),
+                                _p(out["prev_ok"]), _p(out["explored"]), _p(out["err"]))
+        return out
+
+    def stats(self):
+        s = np.zeros(STATS_N, np.float64)
+        self._L.lc_plan_stats(self._h, _p(s), STATS_N)
+        return dict(zip(STATS_NAMES, s.tolist()))
+
+    def close(self):
+        if self._h:
+            self._L.lc_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

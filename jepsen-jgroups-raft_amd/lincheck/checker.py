@@ -1,0 +1,184 @@
+"""jepsen.checker-shaped host API over liblincheck.so.
+
+Mirrors the reference's call sites:
+  (checker/linearizable {:model (model/cas-register) :algorithm :linear})   register.clj:109-111
+  (checker/linearizable {:model (CounterModel. 0) :algorithm :linear})      counter.clj:135-137
+  (independent/checker (checker/compose {:timeline .. :linear ..}))         register.clj:106-111
+A Checker's check(test, history, opts) returns the Knossos-keyed map: "valid?" (True, False
+or "unknown"), "analyzer", and on failure "op", "previous-ok", "last-op", "configs" (<= 10,
+compare as a set), plus "explored" (SURVEY §8(a) contract). Errors raised by the native
+layer propagate, as they would out of Knossos; jepsen's check-safe [ext] turns them into
+{:valid? :unknown :error ...}, which `check_safe` below mirrors.
+"""
+from __future__ import annotations
+
+import traceback
+from typing import Any, Dict, List, Optional, Sequence
+
+from . import _lib
+from . import history as H
+from .model import Model
+
+VALID = {1: True, 0: False, 2: "unknown"}
+ERRORS = {0: None, -4: "malformed history", -5: "too many concurrently pending ops",
+          -6: "model cannot step an op", -7: "frontier exceeded max-configs / device capacity"}
+
+
+def merge_valid(vs: Sequence[Any]):
+    """jepsen.checker/merge-valid [ext]: false beats :unknown beats true."""
+    vs = list(vs)
+    if any(v is False for v in vs):
+        return False
+    if any(v == "unknown" for v in vs):
+        return "unknown"
+    return True
+
+
+class Checker:
+    def check(self, test, history, opts=None) -> Dict[str, Any]:
+        raise NotImplementedError
+
+
+def _op_at(ops: List[Dict[str, Any]], index: int) -> Optional[Dict[str, Any]]:
+    if index < 0:
+        return None
+    for o in ops:
+        if o.get("index") == index:
+            return o
+    return ops[index] if 0 <= index < len(ops) else None
+
+
+def _result_map(ops, r, k, model: Model, configs=None) -> Dict[str, Any]:
+    v = VALID[int(r["valid"][k])]
+    out: Dict[str, Any] = {"valid?": v, "analyzer": "linear",
+                           "explored": int(r["explored"][k])}
+    err = ERRORS.get(int(r["err"][k]))
+    if err:
+        out["error"] = err
+    if v is False:
+        out["op"] = _op_at(ops, int(r["fail_idx"][k]))
+        out["previous-ok"] = _op_at(ops, int(r["prev_ok"][k]))
+        out["last-op"] = out["previous-ok"]
+        out["invocation"] = _op_at(ops, int(r["fail_inv"][k]))
+        if configs is not None:
+            cfgs, pending = configs
+            out["configs"] = [{"model": {"value": s}, "linearized": list(lin),
+                               "pending": pending} for (s, lin) in cfgs]
+    return out
+
+
+class Linearizable(Checker):
+    """(checker/linearizable {:model m :algorithm :linear}) on the GPU."""
+
+    def __init__(self, opts: Dict[str, Any]):
+        m = opts.get("model")
+        if not isinstance(m, Model):
+            raise ValueError("model must be lincheck.model.cas_register() or CounterModel(v)")
+        alg = opts.get("algorithm", "linear")
+        if str(alg).lstrip(":") not in ("linear", "competition", "wgl"):
+            raise ValueError(f"unknown algorithm {alg!r}")
+        self.model = m
+        self.n_gpus = int(opts.get("gpus", 1))
+        self.max_configs = int(opts.get("max-configs", 0))
+        self.report_configs = bool(opts.get("configs", True))
+
+    def check_many(self, h: H.History, ops_per_hist=None) -> List[Dict[str, Any]]:
+        r = _lib.check(self.model.kind, self.model.init_value, h, self.n_gpus, self.max_configs)
+        outs = []
+        for k in range(h.n_hist):
+            ops = ops_per_hist[k] if ops_per_hist is not None else h.to_ops(k)
+            cfg = None
+            if self.report_configs and r["valid"][k] == 0:
+                cfg = _lib.failure_configs(k, 10)
+            outs.append(_result_map(ops, r, k, self.model, cfg))
+        return outs
+
+    def check(self, test, history, opts=None) -> Dict[str, Any]:
+        ops = [o for o in history if H.client_op(o)]
+        h = H.encode(ops)
+        return self.check_many(h, [h.to_ops(0)])[0] if h.n else \
+            {"valid?": True, "analyzer": "linear", "explored": 0}
+
+
+def linearizable(opts: Dict[str, Any]) -> Linearizable:
+    return Linearizable(opts)
+
+
+class Compose(Checker):
+    """jepsen.checker/compose [ext]: run each checker, merge :valid?."""
+
+    def __init__(self, checkers: Dict[str, Checker]):
+        self.checkers = checkers
+
+    def check(self, test, history, opts=None):
+        res = {k: c.check(test, history, opts) for k, c in self.checkers.items()}
+        res["valid?"] = merge_valid(r["valid?"] for r in res.values())
+        return res
+
+
+def compose(checkers: Dict[str, Checker]) -> Compose:
+    return Compose(checkers)
+
+
+class Independent(Checker):
+    """jepsen.independent/checker [ext] (register.clj:106): split by key, check every key.
+    All keys whose inner checker is a Linearizable go down in ONE lc_check call (the GPU
+    batches them); results come back as {"valid?", "results": {k: r}, "failures": [k ...]}."""
+
+    def __init__(self, inner: Checker):
+        self.inner = inner
+
+    def _lin(self) -> Optional[Linearizable]:
+        if isinstance(self.inner, Linearizable):
+            return self.inner
+        if isinstance(self.inner, Compose):
+            lins = [c for c in self.inner.checkers.values() if isinstance(c, Linearizable)]
+            return lins[0] if len(lins) == 1 else None
+        return None
+
+    def check(self, test, history, opts=None):
+        h = H.subhistories(history)
+        lin = self._lin()
+        results: Dict[Any, Dict[str, Any]] = {}
+        if lin is not None and h.n_hist:
+            rs = lin.check_many(h)
+            for k, key in enumerate(h.keys):
+                if isinstance(self.inner, Compose):
+                    name = [n for n, c in self.inner.checkers.items() if c is lin][0]
+                    r = {name: rs[k]}
+                    for n, c in self.inner.checkers.items():
+                        if c is not lin:
+                            r[n] = c.check(test, h.to_ops(k), opts)
+                    r["valid?"] = merge_valid(x["valid?"] for x in r.values())
+                else:
+                    r = rs[k]
+                results[key] = r
+        else:
+            for k, key in enumerate(h.keys or []):
+                results[key] = self.inner.check(test, h.to_ops(k), opts)
+        failures = [k for k, r in results.items() if r["valid?"] is not True]
+        return {"valid?": merge_valid(r["valid?"] for r in results.values()) if results else True,
+                "results": results, "failures": failures}
+
+
+def independent_checker(inner: Checker) -> Independent:
+    return Independent(inner)
+
+
+def check_safe(checker: Checker, test, history, opts=None):
+    """jepsen.checker/check-safe [ext]: exceptions become {:valid? :unknown :error ...}."""
+    try:
+        return checker.check(test, history, opts)
+    except Exception as e:  # noqa: BLE001 — mirrors check-safe's catch-all
+        return {"valid?": "unknown", "error": "".join(traceback.format_exception_only(type(e), e))}
+
+
+class Noop(Checker):
+    """Stand-in for (timeline/html): rendering is out of scope; always valid."""
+
+    def check(self, test, history, opts=None):
+        return {"valid?": True}
+
+
+def timeline_html() -> Noop:
+    return Noop()

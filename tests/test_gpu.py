@@ -1,0 +1,231 @@
+"""GPU parity tests: the HIP search (through the C-ABI) against the CPU oracle on the same
+seeded inputs, against the committed golden KATs, and — at BASELINE sizes — through
+size-independent properties (determinism, perturbation detection, n_gpus invariance)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from brute import literal_search
+from lincheck import _lib, checker, history as H, model, synth
+
+pytestmark = pytest.mark.gpu
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kats.json")))
+KIND = {"cas-register": 1, "counter": 2}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if _lib.load().lc_device_count() < 1:
+        pytest.fail("no HIP device on a GPU run: the checker has no CPU fallback")
+
+
+def _cmp(got, exp, k=0, what=""):
+    assert int(got["valid"][k]) == exp["valid"], (what, k, got["valid"][k], exp)
+    assert int(got["fail_idx"][k]) == exp["fail_idx"], (what, k, got["fail_idx"][k], exp)
+    assert int(got["fail_inv"][k]) == exp["fail_inv_idx"], (what, k)
+    assert int(got["prev_ok"][k]) == exp["prev_ok_idx"], (what, k)
+    if exp["valid"] != 2:
+        assert int(got["explored"][k]) == exp["explored"], (what, k, got["explored"][k], exp)
+
+
+@pytest.mark.parametrize("kat", GOLD, ids=[k["name"] for k in GOLD])
+def test_gpu_kats(kat):
+    h = H.encode(kat["history"])
+    g = _lib.check(KIND[kat["model"]], 0, h)
+    assert int(g["valid"][0]) == (1 if kat["valid"] else 0)
+    assert int(g["fail_idx"][0]) == kat["fail_idx"]
+    if kat["prev_ok_idx"] is not None:
+        assert int(g["prev_ok"][0]) == kat["prev_ok_idx"]
+    if kat["explored"] is not None:
+        assert int(g["explored"][0]) == kat["explored"]
+
+
+def test_gpu_kats_batched():
+    """All KATs of one model in one call: batching must not change any answer."""
+    for m in ("cas-register", "counter"):
+        kats = [k for k in GOLD if k["model"] == m]
+        h = H.concat([H.encode(k["history"]) for k in kats])
+        g = _lib.check(KIND[m], 0, h)
+        for i, k in enumerate(kats):
+            assert int(g["valid"][i]) == (1 if k["valid"] else 0), k["name"]
+            assert int(g["fail_idx"][i]) == k["fail_idx"], k["name"]
+
+
+@pytest.mark.parametrize("m", ["cas-register", "counter"])
+def test_gpu_random_small_vs_oracle(m):
+    rng = random.Random(11)
+    gen = synth.gen_register if m == "cas-register" else synth.gen_counter
+    hs = [gen(rng.randint(1, 40), rng.randint(1, 6), 0.2, 4000 + t, invalid=(t % 2 == 1))
+          for t in range(300)]
+    h = H.concat(hs)
+    g = _lib.check(KIND[m], 0, h)
+    exp = oracle.check_many(m, h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, m)
+    assert any(e["valid"] == 0 for e in exp) and any(e["valid"] == 1 for e in exp)
+
+
+def test_gpu_c1_vs_oracle():
+    """BASELINE config C1: 10 keys x 200 ops, 5 clients."""
+    h = synth.gen_config("c1")
+    g = _lib.check(1, 0, h)
+    exp = oracle.check_many("cas-register", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, "c1")
+
+
+def test_gpu_c3_subset_vs_oracle():
+    """C3 shape (1k ops/key, 5 clients, p_info 0.01) on 24 keys, 4 perturbed."""
+    h = synth.gen_register_keys(24, 1000, 5, 0.01, config_id=3, invalid_keys=(2, 5, 11, 17))
+    g = _lib.check(1, 0, h)
+    exp = oracle.check_many("cas-register", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, "c3-subset")
+
+
+def test_gpu_c2_scaled_vs_oracle():
+    """C2 shape (1 key, 16 clients, p_info 0.002): deep frontier, spills the LDS tables."""
+    h = synth.gen_register(1500, 16, 0.002, synth.seed_for(2, 0))
+    g = _lib.check(1, 0, h)
+    _cmp(g, oracle.check_one("cas-register", h), 0, "c2-scaled")
+
+
+def test_gpu_counter_vs_oracle():
+    hs = [synth.gen_counter(400, 6, 0.005, 9000 + t, invalid=(t % 3 == 0)) for t in range(12)]
+    h = H.concat(hs)
+    g = _lib.check(2, 0, h)
+    exp = oracle.check_many("counter", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, "counter")
+
+
+def test_gpu_counter_init_value():
+    h = synth.gen_counter(200, 4, 0.0, 5)
+    for init in (0, 7, -3):
+        g = _lib.check(2, init, h)
+        _cmp(g, oracle.check_one("counter", h, init_value=init), 0, f"init={init}")
+
+
+def test_gpu_failure_configs_match_oracle():
+    found = 0
+    for t in range(30):
+        h = synth.gen_register(80, 4, 0.1, 9000 + t, invalid=True)
+        g = _lib.check(1, 0, h)
+        e = oracle.check_one("cas-register", h, with_configs=True)
+        assert int(g["valid"][0]) == e["valid"]
+        if e["valid"] != 0:
+            continue
+        cfgs, pending = _lib.failure_configs(0, 1 << 12)
+        assert sorted(pending) == sorted(e["pending_inv_idx"])
+        assert set(cfgs) == e["fail_configs"]
+        assert len(cfgs) == len(e["fail_configs"])
+        found += 1
+    assert found > 5
+
+
+def test_gpu_counter_bounds_vs_oracle():
+    for t in range(40):
+        h = synth.gen_counter(300, 5, 0.05, 600 + t, invalid=(t % 2 == 0))
+        ok, bad = _lib.counter_bounds(0, h)
+        eok, ebad = oracle.counter_bounds(h)
+        assert bool(ok[0]) == eok and int(bad[0]) == ebad
+
+
+def test_gpu_counter_bounds_c5_full_size():
+    """C5 size (1M ops): the scan must accept the linearizable history and reject a
+    perturbed read (size-independent property: soundness + detection)."""
+    h = synth.gen_config("c5")
+    ok, bad = _lib.counter_bounds(0, h)
+    eok, ebad = oracle.counter_bounds(h)
+    assert bool(ok[0]) and eok
+    # perturb one read far outside any window
+    reads = np.nonzero((h.type == 1) & (h.f == 0))[0]
+    j = reads[len(reads) // 2]
+    h.v0[j] += 10 ** 6
+    ok, bad = _lib.counter_bounds(0, h)
+    eok, ebad = oracle.counter_bounds(h)
+    assert not ok[0] and not eok and int(bad[0]) == ebad
+
+
+def test_gpu_errors_are_unknown():
+    bad = H.encode([{"process": 0, "type": "ok", "f": "read", "value": 1}])
+    g = _lib.check(1, 0, bad)
+    assert int(g["valid"][0]) == 2 and int(g["err"][0]) == -4
+    wrong_f = H.encode([{"process": 0, "type": "invoke", "f": "cas", "value": [1, 2]},
+                        {"process": 0, "type": "ok", "f": "cas", "value": [1, 2]}])
+    g = _lib.check(2, 0, wrong_f)
+    assert int(g["valid"][0]) == 2 and int(g["err"][0]) == -6
+    ovf = H.encode([{"process": 0, "type": "invoke", "f": "add", "value": 2 ** 62},
+                    {"process": 0, "type": "ok", "f": "add", "value": 2 ** 62},
+                    {"process": 1, "type": "invoke", "f": "add", "value": 2 ** 62},
+                    {"process": 1, "type": "ok", "f": "add", "value": 2 ** 62}])
+    g = _lib.check(2, 0, ovf)
+    e = oracle.check_one("counter", ovf)
+    assert e["valid"] == 2 and int(g["valid"][0]) == 2 and int(g["err"][0]) == -6
+
+
+def test_gpu_deterministic_and_plan_reuse():
+    h = synth.gen_register_keys(64, 500, 5, 0.01, config_id=7, invalid_keys=(9,))
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    r1 = p.results()
+    p.run()
+    r2 = p.results()
+    for k in r1:
+        assert np.array_equal(r1[k], r2[k]), k
+    r3 = _lib.check(1, 0, h)
+    for k in r1:
+        assert np.array_equal(r1[k], r3[k]), k
+    s = p.stats()
+    assert s["kernel_ms"] > 0 and s["alg_bytes"] > 0 and s["closure_new"] == r1["explored"].sum()
+    p.close()
+
+
+def test_gpu_c3_full_size_properties():
+    """C3 at full size (1k keys x 1k ops): every linearizable key verifies, the perturbed
+    keys the oracle calls invalid are exactly the ones the GPU calls invalid (checked on a
+    sample), and n_gpus does not change answers."""
+    h = synth.gen_register_keys(1000, 1000, 5, 0.01, config_id=3, invalid_keys=(1, 500, 999))
+    g = _lib.check(1, 0, h)
+    assert np.all(g["err"] == 0)
+    sample = [0, 1, 2, 499, 500, 501, 998, 999]
+    exp = oracle.check_many("cas-register", h.select(sample))
+    for i, k in enumerate(sample):
+        _cmp(g, exp[i], k, "c3-sample")
+    clean = np.ones(1000, bool)
+    clean[[1, 500, 999]] = False
+    assert np.all(g["valid"][clean] == 1)
+    g2 = _lib.check(1, 0, h, n_gpus=0)
+    for k in g:
+        assert np.array_equal(g[k], g2[k])
+
+
+def test_checker_api_register_independent():
+    ops = []
+    idx = 0
+    for key in range(3):
+        for (p, t, f, v) in [(0, "invoke", "write", 1), (0, "ok", "write", 1),
+                             (1, "invoke", "read", None), (1, "ok", "read", 1 if key != 1 else 2)]:
+            ops.append({"process": p + 10 * key, "type": t, "f": f, "value": H.tuple_(key, v),
+                        "index": idx})
+            idx += 1
+    c = checker.independent_checker(checker.compose({
+        "timeline": checker.timeline_html(),
+        "linear": checker.linearizable({"model": model.cas_register(), "algorithm": "linear"})}))
+    r = c.check({}, ops, {})
+    assert r["valid?"] is False and r["failures"] == [1]
+    assert r["results"][0]["valid?"] is True
+    lin = r["results"][1]["linear"]
+    assert lin["valid?"] is False and lin["op"]["index"] == 7 and lin["previous-ok"]["index"] == 5
+    assert lin["configs"] and all(cfg["model"]["value"] == 1 for cfg in lin["configs"])
+
+
+def test_checker_api_counter_kats():
+    for kat in [k for k in GOLD if k["model"] == "counter" and k["name"].startswith("counter_")]:
+        c = checker.linearizable({"model": model.CounterModel(0), "algorithm": "linear"})
+        r = c.check({}, kat["history"], {})
+        assert r["valid?"] is kat["valid"], kat["name"]

@@ -1,0 +1,135 @@
+"""Oracle pinning: the reference's golden vectors, hand KATs, and two independent
+restatements (brute-force linearization search, literal frozenset search)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from brute import brute_first_failure, brute_valid, literal_search
+from lincheck import history as H
+from lincheck import synth
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "kats.json")
+KATS = json.load(open(GOLD))
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+def test_oracle_kats(kat):
+    h = H.encode(kat["history"])
+    r = oracle.check_one(kat["model"], h)
+    assert r["valid"] == (1 if kat["valid"] else 0), r
+    assert r["fail_idx"] == kat["fail_idx"]
+    if kat["prev_ok_idx"] is not None:
+        assert r["prev_ok_idx"] == kat["prev_ok_idx"]
+    if kat["explored"] is not None:
+        assert r["explored"] == kat["explored"], r
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["name"] for k in KATS])
+def test_brute_agrees_with_kats(kat):
+    assert brute_valid(kat["model"], kat["history"]) == kat["valid"]
+    lit = literal_search(kat["model"], kat["history"])
+    assert lit["valid"] == kat["valid"]
+    if kat["explored"] is not None:
+        assert lit["explored"] == kat["explored"]
+
+
+def _small_random(model, seed, n_ops, clients, p_info, invalid):
+    g = synth.gen_register if model == "cas-register" else synth.gen_counter
+    return g(n_ops, clients, p_info, seed, invalid=invalid)
+
+
+@pytest.mark.parametrize("model", ["cas-register", "counter"])
+def test_oracle_vs_brute_random(model):
+    rng = random.Random(7)
+    checked = 0
+    for t in range(120):
+        n_ops = rng.randint(1, 7)
+        h = _small_random(model, 1000 + t, n_ops, rng.randint(1, 4), 0.3, invalid=(t % 2 == 1))
+        ops = h.to_ops()
+        r = oracle.check_one(model, h)
+        exp_valid = brute_valid(model, ops)
+        assert r["valid"] == (1 if exp_valid else 0), (ops, r)
+        ff = brute_first_failure(model, ops)
+        assert r["fail_idx"] == (ff if ff < 0 else int(h.index[ff])), (ops, r)
+        lit = literal_search(model, ops)
+        assert lit["explored"] == r["explored"], (ops, r, lit)
+        assert lit["max_frontier"] == r["max_frontier"]
+        checked += 1
+    assert checked == 120
+
+
+@pytest.mark.parametrize("model", ["cas-register", "counter"])
+def test_oracle_vs_literal_medium(model):
+    """Larger random histories (no brute force): the literal restatement must agree on
+    verdict, failing index, explored count and max frontier."""
+    for t in range(12):
+        g = synth.gen_register if model == "cas-register" else synth.gen_counter
+        h = g(60, 4, 0.05, 5000 + t, invalid=(t % 3 == 2))
+        ops = h.to_ops()
+        r = oracle.check_one(model, h)
+        lit = literal_search(model, ops)
+        assert r["valid"] == (1 if lit["valid"] else 0)
+        assert r["fail_idx"] == lit["fail_pos"]
+        assert r["explored"] == lit["explored"]
+        assert r["max_frontier"] == lit["max_frontier"]
+
+
+def test_oracle_failure_configs_match_literal():
+    for t in range(40):
+        h = synth.gen_register(40, 4, 0.1, 9000 + t, invalid=True)
+        ops = h.to_ops()
+        r = oracle.check_one("cas-register", h, with_configs=True)
+        lit = literal_search("cas-register", ops)
+        if not lit["valid"]:
+            exp = set()
+            pre = H.from_columns([], [], [], [], [], [], [])
+            for (s, lin) in lit["frontier"]:
+                inv_idx = tuple(sorted(ops[_inv_pos(ops, k)]["index"] for k in lin))
+                exp.add((None if s == ("nil",) else s, inv_idx))
+            assert r["fail_configs"] == exp
+
+
+def _inv_pos(ops, k):
+    # k is the op ordinal in brute.preprocess order (non-failed invocations)
+    from brute import preprocess
+    return preprocess(ops)[k]["inv"]
+
+
+def test_errors_are_unknown():
+    # completion without invocation
+    h = H.encode([{"process": 0, "type": "ok", "f": "read", "value": 1}])
+    assert oracle.check_one("cas-register", h)["valid"] == 2
+    # unknown :f for the counter model (condp throws, counter.clj:102)
+    h = H.encode([{"process": 0, "type": "invoke", "f": "write", "value": 1},
+                  {"process": 0, "type": "ok", "f": "write", "value": 1}])
+    assert oracle.check_one("counter", h)["valid"] == 2
+    # max_configs exceeded -> unknown
+    h = synth.gen_register(200, 8, 0.2, 77)
+    assert oracle.check_one("cas-register", h, max_configs=1)["valid"] == 2
+
+
+def test_check_many_matches_single():
+    h = synth.gen_register_keys(16, 100, 5, 0.02, config_id=1)
+    many = oracle.check_many("cas-register", h, n_threads=4)
+    for k in range(h.n_hist):
+        assert many[k] == oracle.check_one("cas-register", h.sub(k))
+
+
+def test_counter_bounds_sound():
+    """The bounds filter never rejects a linearizable history and agrees with brute force
+    whenever it rejects."""
+    rejected = 0
+    for t in range(200):
+        h = synth.gen_counter(8, 3, 0.2, 300 + t, invalid=(t % 2 == 1))
+        ok, bad = oracle.counter_bounds(h)
+        lin = brute_valid("counter", h.to_ops())
+        if lin:
+            assert ok
+        if not ok:
+            rejected += 1
+            assert not lin
+    assert rejected > 10
