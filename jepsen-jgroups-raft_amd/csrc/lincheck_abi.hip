@@ -12,6 +12,7 @@
 #include <climits>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -22,6 +23,7 @@
 #include "../../include/lincheck.h"
 #include "bounds.hpp"
 #include "encode.hpp"
+#include "keys.hpp"
 #include "search.hpp"
 
 namespace lc {
@@ -47,6 +49,15 @@ void set_err(char* err, int32_t len, const char* fmt, ...) {
 std::mutex& device_mutex(int dev) {
   static std::mutex mus[64];
   return mus[dev & 63];
+}
+
+bool debug() {
+  static int d = -1;
+  if (d < 0) {
+    const char* e = getenv("LC_DEBUG");
+    d = (e && *e && *e != '0') ? 1 : 0;
+  }
+  return d == 1;
 }
 
 int bits_for(int64_t n) {  // bits to represent values 0..n-1
@@ -88,28 +99,41 @@ struct lc_plan {
   int64_t max_configs = 0;
   Encoded enc;
   std::string last_error;
-  // batches of histories sharing one packed key layout
+  // batches of histories (global ids) sharing one packed key layout (grid kernel)
   struct Batch {
-    int h0, h1, mask_bits, state_bits, hist_bits;
+    std::vector<int> hs;
+    int mask_bits, state_bits, hist_bits;
   };
   std::vector<Batch> batches;
-  int nwg = 0, cell_cap = 256, f_cap = 16384, spill_log = 14;
+  int path = 0;  // 0 auto, 1 keys kernel first, 2 grid kernel only
+  int nwg = 0, cell_cap = 256, f_cap = 65536, spill_log = 17;
+  int64_t ovf_cap = 1 << 18;
+  int knwg = 0;
+  int64_t kfcap = 1 << 18, klcap = 1 << 18;
+  int kspill_log = 18;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // device copies of the encoded history
   DevArray d_step_off, d_step_slot, d_inv_off, d_inv_slot, d_inv_kind, d_inv_a, d_inv_b, d_init;
-  // per-history work state (sized for the largest batch)
+  DevArray d_beg, d_end, d_kshift, d_kbits, d_order, d_queue;  // keys kernel (all histories)
+  DevArray d_bbeg, d_bend, d_binit;                           // grid batch gathers
+  // per-history work state
   DevArray d_live, d_opk, d_opa, d_opb, d_status, d_fail, d_nonempty, d_explored;
-  // per-owner storage
-  DevArray d_flist, d_fcount, d_cells, d_cellcnt, d_spill, d_spillpos;
-  DevArray d_bar, d_produced, d_running, d_flags, d_stats;
-  bool spill_clean = false;
+  // grid-kernel per-owner storage
+  DevArray d_flist, d_fcount, d_cells, d_cellcnt, d_ovf, d_ovfcnt, d_spill, d_spillpos;
+  DevArray d_bar, d_produced, d_running, d_flags, d_stats, d_stamps;
+  // keys-kernel per-workgroup storage
+  DevArray d_kscratch, d_kspill, d_kspillpos, d_kstatus, d_kfail, d_kexplored;
+  bool spill_clean = false, kspill_clean = false;
   // results
   std::vector<int32_t> status, fail_step;
   std::vector<unsigned long long> explored;
   double stats[LC_STATS_N] = {0};
-  int32_t max_t = INT32_MAX;  // failure-frontier dump mode
+  int32_t max_t = INT32_MAX;  // failure-frontier dump mode (grid kernel)
   int64_t entry_bytes() const { return model == LC_MODEL_CAS_REGISTER ? 8 : 16; }
+  int state_bits_of(int h) const {
+    return model == LC_MODEL_CAS_REGISTER ? bits_for(enc.n_states[h]) : 0;
+  }
 
   ~lc_plan() {
     if (ev0) hipEventDestroy(ev0);
@@ -117,37 +141,36 @@ struct lc_plan {
     if (stream) hipStreamDestroy(stream);
   }
 
-  void make_batches() {
-    batches.clear();
-    const int n = enc.n_hist;
-    for (int h = 0; h < n; ++h) {  // a key must hold [state | mask] of one history in 63 bits
-      const int sb = model == LC_MODEL_CAS_REGISTER ? bits_for(enc.n_states[h]) : 0;
-      if (!enc.err[h] && enc.live_max[h] + sb > 63) {
+  void flag_wide() {
+    for (int h = 0; h < enc.n_hist; ++h) {  // [state | mask] of one history must fit 63 bits
+      if (!enc.err[h] && enc.live_max[h] + state_bits_of(h) > 63) {
         enc.err[h] = LC_H_WIDE;
         enc.errmsg[h] = "pending ops + state bits exceed the 63-bit packed config";
       }
     }
-    int h = 0;
-    while (h < n) {
-      Batch b{h, h, 1, 0, 0};
+  }
+
+  void make_batches(const std::vector<int>& ids) {
+    batches.clear();
+    size_t i = 0;
+    while (i < ids.size()) {
+      Batch b;
       int mb = 1, sb = 0;
-      int e = h;
-      while (e < n && e - h < HMAX) {
-        int mb2 = std::max(mb, enc.live_max[e]);
-        int sb2 = model == LC_MODEL_CAS_REGISTER ? std::max(sb, bits_for(enc.n_states[e])) : 0;
-        int hb2 = bits_for(e - h + 1);
-        if (mb2 + sb2 + hb2 > 63) break;
+      while (i < ids.size() && (int)b.hs.size() < HMAX) {
+        const int h = ids[i];
+        int mb2 = std::max(mb, enc.live_max[h]);
+        int sb2 = std::max(sb, state_bits_of(h));
+        int hb2 = bits_for((int64_t)b.hs.size() + 1);
+        if (!b.hs.empty() && mb2 + sb2 + hb2 > 63) break;
         mb = mb2;
         sb = sb2;
-        ++e;
+        b.hs.push_back(h);
+        ++i;
       }
-      if (e == h) e = h + 1;  // a single history always forms a batch (encoder bounds it)
-      b.h1 = e;
       b.mask_bits = mb;
       b.state_bits = sb;
-      b.hist_bits = bits_for(e - h);
-      batches.push_back(b);
-      h = e;
+      b.hist_bits = bits_for((int64_t)b.hs.size());
+      batches.push_back(std::move(b));
     }
   }
 
@@ -164,16 +187,40 @@ struct lc_plan {
     if (!ev0) HIP_TRY(hipEventCreate(&ev0));
     if (!ev1) HIP_TRY(hipEventCreate(&ev1));
     nwg = search_grid_size(model);
-    if (nwg <= 0) {
-      last_error = "search kernel cannot be resident (occupancy 0)";
+    knwg = keys_grid_size(model);
+    if (nwg <= 0 || knwg <= 0) {
+      last_error = "search kernels cannot be resident (occupancy 0)";
       return LC_E_DEVICE;
     }
+    const char* e = getenv("LC_PATH");
+    if (e && !strcmp(e, "keys")) path = 1;
+    if (e && !strcmp(e, "grid")) path = 2;
+    // test hooks: shrink the keys kernel's per-workgroup capacities to force the fallback
+    if ((e = getenv("LC_KCAP")) && atoll(e) > 0) kfcap = klcap = atoll(e);
+    // test hooks: tiny cells / overflow buckets exercise the overflow and regrow paths
+    if ((e = getenv("LC_CELLCAP")) && atoi(e) > 0) cell_cap = atoi(e);
+    if ((e = getenv("LC_OVFCAP")) && atoll(e) > 0) ovf_cap = atoll(e);
     return 0;
   }
 
   int upload_encoded() {
-    std::vector<int64_t> init(enc.n_hist);
-    for (int h = 0; h < enc.n_hist; ++h) init[h] = model == LC_MODEL_CAS_REGISTER ? 0 : enc.init_value;
+    flag_wide();
+    const int n = enc.n_hist;
+    std::vector<int64_t> init(n);
+    std::vector<int32_t> beg(n), end(n), order(n);
+    std::vector<int8_t> ksh(n), kbi(n);
+    std::vector<double> cost(n);
+    for (int h = 0; h < n; ++h) {
+      init[h] = model == LC_MODEL_CAS_REGISTER ? 0 : enc.init_value;
+      beg[h] = enc.step_off[h];
+      end[h] = enc.step_off[h + 1];
+      ksh[h] = (int8_t)enc.live_max[h];
+      kbi[h] = (int8_t)state_bits_of(h);
+      order[h] = h;
+      // heaviest first: frontier width grows with the pending window
+      cost[h] = (double)enc.n_steps(h) * (1.0 + enc.live_max[h]) * (1.0 + enc.live_max[h]);
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
     int rc;
     if ((rc = upload(d_step_off, enc.step_off))) return rc;
     if ((rc = upload(d_step_slot, enc.step_slot))) return rc;
@@ -183,10 +230,16 @@ struct lc_plan {
     if ((rc = upload(d_inv_a, enc.inv_a))) return rc;
     if ((rc = upload(d_inv_b, enc.inv_b))) return rc;
     if ((rc = upload(d_init, init))) return rc;
+    if ((rc = upload(d_beg, beg))) return rc;
+    if ((rc = upload(d_end, end))) return rc;
+    if ((rc = upload(d_kshift, ksh))) return rc;
+    if ((rc = upload(d_kbits, kbi))) return rc;
+    if ((rc = upload(d_order, order))) return rc;
+    HIP_TRY(d_queue.ensure(8));
     return 0;
   }
 
-  int ensure_work(int nh) {
+  int ensure_grid(int nh) {
     HIP_TRY(d_live.ensure(2ull * nh * 8));
     HIP_TRY(d_opk.ensure(2ull * nh * 64));
     HIP_TRY(d_opa.ensure(2ull * nh * 64 * 8));
@@ -195,11 +248,16 @@ struct lc_plan {
     HIP_TRY(d_fail.ensure((size_t)nh * 4));
     HIP_TRY(d_nonempty.ensure(2ull * nh * 4));
     HIP_TRY(d_explored.ensure((size_t)nh * 8));
+    HIP_TRY(d_bbeg.ensure((size_t)nh * 4));
+    HIP_TRY(d_bend.ensure((size_t)nh * 4));
+    HIP_TRY(d_binit.ensure((size_t)nh * 8));
     const size_t E = (size_t)entry_bytes();
     HIP_TRY(d_flist.ensure(2ull * nwg * f_cap * E));
     HIP_TRY(d_fcount.ensure(2ull * nwg * 4));
     HIP_TRY(d_cells.ensure(2ull * nwg * nwg * cell_cap * E));
     HIP_TRY(d_cellcnt.ensure(2ull * nwg * nwg * 4));
+    HIP_TRY(d_ovf.ensure(2ull * nwg * ovf_cap * E));
+    HIP_TRY(d_ovfcnt.ensure(2ull * nwg * 4));
     size_t sp = (size_t)nwg << spill_log;
     if (d_spill.bytes < sp * 8) {
       HIP_TRY(d_spill.ensure(sp * 8));
@@ -214,14 +272,117 @@ struct lc_plan {
     return 0;
   }
 
-  // run one batch; returns 0, LC_E_* on hard errors, 1 when capacities must grow
+  void add_stats(const unsigned long long* ss) {
+    stats[1] += 1;
+    stats[2] += (double)ss[SS_STEPS];
+    stats[3] += (double)ss[SS_PHASES];
+    stats[4] += (double)ss[SS_FIN];
+    stats[5] += (double)ss[SS_CAND];
+    stats[6] += (double)ss[SS_FOUT];
+    stats[11] += (double)ss[SS_SPILL];
+  }
+
+  // keys kernel over every history; returns 0 or LC_E_*
+  int run_keys(float* ms) {
+    const int n = enc.n_hist;
+    const size_t E = (size_t)entry_bytes();
+    HIP_TRY(d_kscratch.ensure((size_t)knwg * (2 * kfcap + 2 * klcap) * E));
+    const size_t sp = (size_t)knwg << kspill_log;
+    if (d_kspill.bytes < sp * 8) {
+      HIP_TRY(d_kspill.ensure(sp * 8));
+      kspill_clean = false;
+    }
+    HIP_TRY(d_kspillpos.ensure(sp * 4));
+    HIP_TRY(d_kstatus.ensure((size_t)std::max(n, 1) * 4));
+    HIP_TRY(d_kfail.ensure((size_t)std::max(n, 1) * 4));
+    HIP_TRY(d_kexplored.ensure((size_t)std::max(n, 1) * 8));
+    HIP_TRY(d_stats.ensure(SS_N * 8));
+    std::vector<int32_t> st0(n);
+    for (int h = 0; h < n; ++h) st0[h] = enc.err[h] ? ST_SKIP : ST_RUNNING;
+    if (n) HIP_TRY(hipMemcpyAsync(d_kstatus.p, st0.data(), n * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemsetAsync(d_queue.p, 0, 8, stream));
+    HIP_TRY(hipMemsetAsync(d_stats.p, 0, SS_N * 8, stream));
+    if (!kspill_clean) {
+      HIP_TRY(hipMemsetAsync(d_kspill.p, 0xff, sp * 8, stream));
+      kspill_clean = true;
+    }
+    KeysParams p{};
+    p.n_hist = n;
+    p.model = model;
+    p.kshift = d_kshift.as<int8_t>();
+    p.kbits = d_kbits.as<int8_t>();
+    p.fcap = kfcap;
+    p.lcap = klcap;
+    p.spill_log = kspill_log;
+    p.step_beg = d_beg.as<int32_t>();
+    p.step_end = d_end.as<int32_t>();
+    p.step_slot = d_step_slot.as<uint8_t>();
+    p.inv_off = d_inv_off.as<int64_t>();
+    p.inv_slot = d_inv_slot.as<uint8_t>();
+    p.inv_kind = d_inv_kind.as<uint8_t>();
+    p.inv_a = d_inv_a.as<int64_t>();
+    p.inv_b = d_inv_b.as<int64_t>();
+    p.init_st = d_init.as<int64_t>();
+    p.order = d_order.as<int32_t>();
+    p.queue = d_queue.as<int32_t>();
+    p.status = d_kstatus.as<int32_t>();
+    p.fail_step = d_kfail.as<int32_t>();
+    p.explored = d_kexplored.as<unsigned long long>();
+    p.scratch = d_kscratch.p;
+    p.spill = d_kspill.as<uint64_t>();
+    p.spill_pos = d_kspillpos.as<uint32_t>();
+    p.stats = d_stats.as<unsigned long long>();
+    const int grid = std::min(knwg, std::max(1, n));
+    HIP_TRY(hipEventRecord(ev0, stream));
+    HIP_TRY(launch_keys(p, grid, stream));
+    HIP_TRY(hipEventRecord(ev1, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
+    *ms += t;
+    std::vector<int32_t> st(n), fs(n);
+    std::vector<unsigned long long> ex(n);
+    if (n) {
+      HIP_TRY(hipMemcpy(st.data(), d_kstatus.p, n * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(fs.data(), d_kfail.p, n * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(ex.data(), d_kexplored.p, n * 8, hipMemcpyDeviceToHost));
+    }
+    unsigned long long ss[SS_N];
+    HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
+    add_stats(ss);
+    int ncap = 0;
+    for (int h = 0; h < n; ++h) {
+      status[h] = st[h];
+      fail_step[h] = fs[h];
+      explored[h] = ex[h];
+      ncap += st[h] == ST_CAPACITY;
+    }
+    if (debug())
+      fprintf(stderr,
+              "[lincheck] keys kernel: %d histories on %d workgroups: %.2f ms, steps=%llu Fin=%llu "
+              "cand=%llu Fout=%llu spill=%llu -> %d over capacity\n",
+              n, grid, t, ss[SS_STEPS], ss[SS_FIN], ss[SS_CAND], ss[SS_FOUT], ss[SS_SPILL], ncap);
+    return 0;
+  }
+
+  // grid kernel on one batch; returns 0, LC_E_* on hard errors, 1/2 when capacities must grow
   int run_batch(const Batch& bt, float* ms) {
-    const int nh = bt.h1 - bt.h0;
-    int rc = ensure_work(nh);
+    const int nh = (int)bt.hs.size();
+    int rc = ensure_grid(nh);
     if (rc) return rc;
-    std::vector<int32_t> st0(nh);
-    for (int i = 0; i < nh; ++i) st0[i] = enc.err[bt.h0 + i] ? ST_SKIP : ST_RUNNING;
+    std::vector<int32_t> st0(nh), beg(nh), end(nh);
+    std::vector<int64_t> init(nh);
+    for (int i = 0; i < nh; ++i) {
+      const int h = bt.hs[i];
+      st0[i] = enc.err[h] ? ST_SKIP : ST_RUNNING;
+      beg[i] = enc.step_off[h];
+      end[i] = enc.step_off[h + 1];
+      init[i] = model == LC_MODEL_CAS_REGISTER ? 0 : enc.init_value;
+    }
     HIP_TRY(hipMemcpyAsync(d_status.p, st0.data(), nh * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_bbeg.p, beg.data(), nh * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_bend.p, end.data(), nh * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_binit.p, init.data(), nh * 8, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemsetAsync(d_live.p, 0, 2ull * nh * 8, stream));
     HIP_TRY(hipMemsetAsync(d_fail.p, 0xff, (size_t)nh * 4, stream));
     HIP_TRY(hipMemsetAsync(d_nonempty.p, 0, 2ull * nh * 4, stream));
@@ -231,6 +392,7 @@ struct lc_plan {
       spill_clean = true;
     }
     HIP_TRY(hipMemsetAsync(d_bar.p, 0, sizeof(GridBar), stream));
+    HIP_TRY(hipMemsetAsync(d_ovfcnt.p, 0, 2ull * nwg * 4, stream));
     HIP_TRY(hipMemsetAsync(d_produced.p, 0, 32, stream));
     HIP_TRY(hipMemsetAsync(d_running.p, 0, 16, stream));
     HIP_TRY(hipMemsetAsync(d_flags.p, 0, FL_N * 4, stream));
@@ -247,14 +409,15 @@ struct lc_plan {
     p.spill_log = spill_log;
     p.max_t = max_t;
     p.model = model;
-    p.step_off = d_step_off.as<int32_t>() + bt.h0;
+    p.step_beg = d_bbeg.as<int32_t>();
+    p.step_end = d_bend.as<int32_t>();
     p.step_slot = d_step_slot.as<uint8_t>();
     p.inv_off = d_inv_off.as<int64_t>();
     p.inv_slot = d_inv_slot.as<uint8_t>();
     p.inv_kind = d_inv_kind.as<uint8_t>();
     p.inv_a = d_inv_a.as<int64_t>();
     p.inv_b = d_inv_b.as<int64_t>();
-    p.init_st = d_init.as<int64_t>() + bt.h0;
+    p.init_st = d_binit.as<int64_t>();
     p.live = d_live.as<uint64_t>();
     p.op_kind = d_opk.as<uint8_t>();
     p.op_a = d_opa.as<int64_t>();
@@ -267,6 +430,9 @@ struct lc_plan {
     p.fcount = d_fcount.as<uint32_t>();
     p.cells = d_cells.p;
     p.cell_cnt = d_cellcnt.as<uint32_t>();
+    p.ovf = d_ovf.p;
+    p.ovf_cnt = d_ovfcnt.as<uint32_t>();
+    p.ovf_cap = ovf_cap;
     p.spill = d_spill.as<uint64_t>();
     p.spill_pos = d_spillpos.as<uint32_t>();
     p.bar = d_bar.as<GridBar>();
@@ -274,6 +440,12 @@ struct lc_plan {
     p.running = d_running.as<unsigned>();
     p.flags = d_flags.as<int32_t>();
     p.stats = d_stats.as<unsigned long long>();
+    p.stamps = nullptr;
+    if (debug()) {
+      HIP_TRY(d_stamps.ensure((size_t)nwg * 8 * 8));
+      HIP_TRY(hipMemsetAsync(d_stamps.p, 0, (size_t)nwg * 64, stream));
+      p.stamps = d_stamps.as<unsigned long long>();
+    }
 
     HIP_TRY(hipEventRecord(ev0, stream));
     HIP_TRY(launch_search(p, stream));
@@ -285,13 +457,36 @@ struct lc_plan {
 
     int32_t flags[FL_N];
     HIP_TRY(hipMemcpy(flags, d_flags.p, sizeof(flags), hipMemcpyDeviceToHost));
+    unsigned long long ss[SS_N];
+    HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
+    if (debug())
+      fprintf(stderr,
+              "[lincheck] grid batch %d hist bits m%d s%d h%d nwg=%d cell_cap=%d ovf_cap=%lld f_cap=%d "
+              "spill_log=%d: %.2f ms, steps=%llu phases=%llu Fin=%llu cand=%llu Fout=%llu "
+              "spill=%llu flags abort=%d ovf=%d spillfull=%d\n",
+              nh, bt.mask_bits, bt.state_bits, bt.hist_bits, nwg, cell_cap, (long long)ovf_cap, f_cap, spill_log, t,
+              ss[SS_STEPS], ss[SS_PHASES], ss[SS_FIN], ss[SS_CAND], ss[SS_FOUT], ss[SS_SPILL],
+              flags[FL_ABORT], flags[FL_OVERFLOW], flags[FL_SPILL]);
+    if (debug()) {
+      std::vector<unsigned long long> T((size_t)nwg * 8);
+      HIP_TRY(hipMemcpy(T.data(), d_stamps.p, T.size() * 8, hipMemcpyDeviceToHost));
+      double m[8] = {0};
+      for (int w = 0; w < nwg; ++w)
+        for (int i = 0; i < 8; ++i) m[i] += (double)T[(size_t)w * 8 + i] / nwg;
+      const double ph = std::max(1.0, (double)ss[SS_PHASES]);
+      fprintf(stderr,
+              "[lincheck]   mean us per phase (s_memrealtime): barrier %.2f  X-hist %.2f  "
+              "X-expand %.2f  prefix %.2f  process %.2f  publish %.2f  step-end %.2f (phases %.0f)\n",
+              m[0] / ph / 100, m[1] / ph / 100, m[2] / ph / 100, m[3] / ph / 100, m[4] / ph / 100,
+              m[5] / ph / 100, m[6] / ph / 100, ph);
+    }
     if (flags[FL_ABORT]) {
       last_error = "search kernel watchdog: grid barrier timed out";
       return LC_E_INTERNAL;
     }
     if (flags[FL_SPILL]) {
       spill_clean = false;  // a full spill table may hold stale entries
-      return 1 + 1;
+      return 2;
     }
     if (flags[FL_OVERFLOW]) return 1;
 
@@ -300,21 +495,13 @@ struct lc_plan {
     HIP_TRY(hipMemcpy(st.data(), d_status.p, nh * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fs.data(), d_fail.p, nh * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(ex.data(), d_explored.p, nh * 8, hipMemcpyDeviceToHost));
-    unsigned long long ss[SS_N];
-    HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
     for (int i = 0; i < nh; ++i) {
-      status[bt.h0 + i] = st[i];
-      fail_step[bt.h0 + i] = fs[i];
-      explored[bt.h0 + i] = ex[i];
+      const int h = bt.hs[i];
+      status[h] = st[i];
+      fail_step[h] = fs[i];
+      explored[h] = ex[i];
     }
-    stats[1] += 1;
-    stats[2] += (double)ss[SS_STEPS];
-    stats[3] += (double)ss[SS_PHASES];
-    stats[4] += (double)ss[SS_FIN];
-    stats[5] += (double)ss[SS_CAND];
-    stats[6] += (double)ss[SS_FOUT];
-    stats[7] += (double)ss[SS_SNEW];
-    stats[11] += (double)ss[SS_SPILL];
+    add_stats(ss);
     return 0;
   }
 
@@ -324,18 +511,13 @@ struct lc_plan {
     return free_b;
   }
 
-  int run() {
-    int rc;
-    HIP_TRY(hipSetDevice(device));
-    status.assign(enc.n_hist, ST_SKIP);
-    fail_step.assign(enc.n_hist, -1);
-    explored.assign(enc.n_hist, 0);
-    std::fill(stats, stats + LC_STATS_N, 0.0);
-    float ms = 0;
+  int run_grid(const std::vector<int>& ids, float* ms) {
+    make_batches(ids);
     for (size_t bi = 0; bi < batches.size(); ++bi) {
       const Batch& bt = batches[bi];
+      int rc;
       for (int attempt = 0;; ++attempt) {
-        rc = run_batch(bt, &ms);
+        rc = run_batch(bt, ms);
         if (rc <= 0) break;
         // grow what overflowed, bounded by max_configs and free HBM
         const size_t E = (size_t)entry_bytes();
@@ -344,21 +526,47 @@ struct lc_plan {
           spill_log += 2;
           need = ((size_t)nwg << spill_log) * 12;
         } else {
-          cell_cap *= 4;
-          f_cap *= 4;
-          need = 2ull * nwg * nwg * cell_cap * E + 2ull * nwg * f_cap * E;
+          ovf_cap *= 4;
+          f_cap *= 2;
+          need = 2ull * nwg * ovf_cap * E + 2ull * nwg * f_cap * E;
         }
         bool over_cfg = max_configs > 0 && (int64_t)nwg * f_cap > 4 * max_configs;
         if (over_cfg || need > device_budget() * 9 / 10 || attempt > 6 || spill_log > 24) {
           // capacity exhausted: the batch's histories are undecided (Knossos: :unknown)
-          for (int h = bt.h0; h < bt.h1; ++h) status[h] = enc.err[h] ? ST_SKIP : ST_CAPACITY;
+          for (int h : bt.hs) status[h] = enc.err[h] ? ST_SKIP : ST_CAPACITY;
           rc = 0;
           break;
         }
-        d_cells.release();
+        d_ovf.release();
         d_flist.release();
       }
       if (rc < 0) return rc;
+    }
+    return 0;
+  }
+
+  int run() {
+    HIP_TRY(hipSetDevice(device));
+    status.assign(enc.n_hist, ST_SKIP);
+    fail_step.assign(enc.n_hist, -1);
+    explored.assign(enc.n_hist, 0);
+    std::fill(stats, stats + LC_STATS_N, 0.0);
+    float ms = 0;
+    int rc = 0;
+    std::vector<int> grid_ids;
+    const bool keys = max_t == INT32_MAX && path == 1;
+    if (keys) {
+      rc = run_keys(&ms);
+      if (rc) return rc;
+      for (int h = 0; h < enc.n_hist; ++h)
+        if (status[h] == ST_CAPACITY) grid_ids.push_back(h);
+    } else {
+      for (int h = 0; h < enc.n_hist; ++h)
+        if (!enc.err[h]) grid_ids.push_back(h);
+    }
+    if (!grid_ids.empty()) {
+      rc = run_grid(grid_ids, &ms);
+      if (rc) return rc;
     }
     stats[0] = ms;
     stats[7] = 0;
@@ -367,7 +575,7 @@ struct lc_plan {
     // bytes_alg = F_in*C + N_cand*(C+8) + F_out*C
     const double C = stats[8];
     stats[9] = stats[4] * C + stats[5] * (C + 8) + stats[6] * C;
-    stats[10] = nwg;
+    stats[10] = keys ? knwg : nwg;
     return 0;
   }
 
@@ -410,7 +618,6 @@ int plan_build(int device, int model, int64_t init_value, int n_hist, const int6
   p->model = model;
   p->max_configs = max_configs;
   encode(model, init_value, n_hist, hist_off, a, p->enc);
-  p->make_batches();
   int rc = p->init_device();
   if (!rc) rc = p->upload_encoded();
   if (rc) {

@@ -19,66 +19,81 @@
 //                returning op are routed "direct" with MARK)
 //      level ℓ : dedup incoming candidates into S / OUT, expand the new ones
 //    until a phase routes nothing. Grid barriers separate phases.
+#include "device_common.hpp"
 #include "search.hpp"
 
 #include <climits>
 
 namespace lc {
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return x;
-}
+__device__ __forceinline__ uint64_t stamp() { return __builtin_amdgcn_s_memrealtime(); }  // 100 MHz
 
-template <typename T>
-__device__ __forceinline__ T ld_agent(const T* ptr) {
-  return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// sc1 (write-through, L1-bypassing) 8-byte hand-off of cell entries between workgroups
+__device__ __forceinline__ void put_entry(RegEntry* dst, const RegEntry& e) { st_agent(&dst->key, e.key); }
+__device__ __forceinline__ void put_entry(CntEntry* dst, const CntEntry& e) {
+  st_agent(&dst->key, e.key);
+  st_agent((uint64_t*)&dst->st, (uint64_t)e.st);
 }
-template <typename T>
-__device__ __forceinline__ void st_agent(T* ptr, T v) {
-  __hip_atomic_store(ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ RegEntry get_entry(const RegEntry* src) { return RegEntry{ld_agent(&src->key)}; }
+__device__ __forceinline__ CntEntry get_entry(const CntEntry* src) {
+  return CntEntry{ld_agent(&src->key), (int64_t)ld_agent((const uint64_t*)&src->st)};
 }
 
 __device__ __forceinline__ uint32_t owner_of(uint64_t x, uint32_t nwg) {
   return (uint32_t)(((mix64(x) >> 32) * (uint64_t)nwg) >> 32);
 }
 
-// XCD-hierarchy-free counter barrier with an agent-scope release/acquire
-// (MI355X_MICROARCH "barrier-counter"; cdna_hip_programming.md §6 G16). Bounded spin:
-// a stuck barrier raises FL_ABORT instead of hanging the GPU.
-__device__ __forceinline__ bool grid_sync(const SearchParams& p, int* s_abort) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// Grid barrier: two-level arrival counters (8 groups, then the top counter) so at most 32
+// arrivals serialise on one word, and a release generation polled relaxed with s_sleep
+// (MI355X_MICROARCH "barrier-xcd" / "fanin"). `fenced` adds the agent-scope release/acquire
+// (cdna_hip_programming.md §6 G16) for phases that publish plain stores; level phases hand
+// off only sc1 (write-through) stores read back with sc1 loads, so they skip both fences.
+// Bounded spin: a stuck barrier raises FL_ABORT instead of hanging the GPU.
+__device__ __forceinline__ bool grid_sync(const SearchParams& p, int* s_abort, uint64_t* t_bar,
+                                          bool fenced) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its stores
   __syncthreads();
+  const uint64_t t_arrive = stamp();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned g = __hip_atomic_load(&p.bar->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned arrived =
-        __hip_atomic_fetch_add(&p.bar->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == (unsigned)p.nwg - 1) {
-      __hip_atomic_store(&p.bar->count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&p.bar->gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      long spins = 0;
-      while (__hip_atomic_load(&p.bar->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1L << 27)) {
-          __hip_atomic_store(&p.flags[FL_ABORT], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        if ((spins & 1023) == 0 &&
-            __hip_atomic_load(&p.flags[FL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-          break;
+    if (fenced) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    GridBar* bar = p.bar;
+    const unsigned nwg = (unsigned)p.nwg;
+    const unsigned g = ld_agent(&bar->gen);
+    const unsigned grp = blockIdx.x & 7u;
+    const unsigned gsize = (nwg - grp + 7u) >> 3;
+    const unsigned ngroups = nwg < 8u ? nwg : 8u;
+    const unsigned a =
+        __hip_atomic_fetch_add(&bar->grp[grp][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a == gsize - 1) {
+      st_agent(&bar->grp[grp][0], 0u);
+      const unsigned t =
+          __hip_atomic_fetch_add(&bar->top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == ngroups - 1) {
+        st_agent(&bar->top, 0u);
+        __hip_atomic_store(&bar->gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    *s_abort = __hip_atomic_load(&p.flags[FL_ABORT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // watchdog on the 100 MHz constant clock: 20 s without a release aborts the search
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    long spins = 0;
+    while (ld_agent(&bar->gen) == g) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+          st_agent(&p.flags[FL_ABORT], 1);
+          break;
+        }
+        if (ld_agent(&p.flags[FL_ABORT])) break;
+      }
+    }
+    if (fenced) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *s_abort = ld_agent(&p.flags[FL_ABORT]);
   }
   __syncthreads();
+  if (t_bar) *t_bar += stamp() - t_arrive;
   return *s_abort == 0;
 }
 
@@ -107,6 +122,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
   __shared__ unsigned long long sStat[SS_N];
   __shared__ unsigned long long sTotal;
   __shared__ int sAbort;
+  __shared__ uint64_t sSent[1 << SENT_LOG];  // candidate keys routed in this phase (lossy)
 
   const int tid = threadIdx.x;
   const uint32_t wg = blockIdx.x;
@@ -164,14 +180,24 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
     return spill_insert(k | tag);
   };
 
-  // route one item to its owner's cell (parity par)
+  // route one item to its owner's cell (parity par). A key already routed by this workgroup
+  // in this phase is dropped at the source: the owner would discard it as a duplicate.
+  // (cleared every phase; a key is written before its send, which completes in this phase)
   auto route = [&](const E& e, uint64_t rkey, int par) {
+    const uint64_t hk = mix64(e.key);
+    const uint32_t si = (uint32_t)(hk >> 40) & ((1u << SENT_LOG) - 1);
+    if (sSent[si] == e.key) return;
+    sSent[si] = e.key;  // racy overwrite is harmless: a miss only re-sends
     uint32_t dst = owner_of(rkey, nwg);
     uint32_t pos = atomicAdd(&sCnt[dst], 1u);
     if (pos < ccap) {
-      cells[(((size_t)par * nwg + dst) * nwg + wg) * ccap + pos] = e;
-    } else {
-      __hip_atomic_store(&p.flags[FL_OVERFLOW], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      put_entry(&cells[(((size_t)par * nwg + dst) * nwg + wg) * ccap + pos], e);
+    } else {  // this cell is full: reserve a slot in the destination's overflow bucket
+      const uint32_t r = atomicAdd(&p.ovf_cnt[(size_t)par * nwg + dst], 1u);
+      if (r < (uint64_t)p.ovf_cap)
+        put_entry(&((E*)p.ovf)[((size_t)par * nwg + dst) * p.ovf_cap + r], e);
+      else
+        st_agent(&p.flags[FL_OVERFLOW], 1);
     }
   };
 
@@ -218,10 +244,11 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
   // write this phase's per-destination counts, publish the routed total
   auto publish_counts = [&](int par, int phase) {
     __syncthreads();
+    for (int i = tid; i < (1 << SENT_LOG); i += BLOCK) sSent[i] = EMPTY;
     unsigned long long local = 0;
     for (int d = tid; d < (int)nwg; d += BLOCK) {
       const uint32_t c = sCnt[d];
-      p.cell_cnt[((size_t)par * nwg + d) * nwg + wg] = c;
+      st_agent(&p.cell_cnt[((size_t)par * nwg + d) * nwg + wg], (uint32_t)min((size_t)c, ccap));
       local += c;
       sCnt[d] = 0;
     }
@@ -243,6 +270,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
   for (int i = tid; i < HMAX; i += BLOCK) sExpl[i] = 0;
   for (int i = tid; i < HMAX / 32; i += BLOCK) sNE[i] = 0;
   for (int i = tid; i < WGMAX; i += BLOCK) sCnt[i] = 0;
+  for (int i = tid; i < (1 << SENT_LOG); i += BLOCK) sSent[i] = EMPTY;
   if (tid < SS_N) sStat[tid] = 0;
   if (tid == 0) {
     sFcount[0] = sFcount[1] = 0;
@@ -252,12 +280,13 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
   }
   __syncthreads();
   const int gtid = (int)wg * BLOCK + tid;
+  uint64_t T[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // phase stamps (s_memtime cycles), thread 0 reports
   // slot tables for step 0 (buffer 0); buffer 1 starts empty (= state before step 0)
   if (gtid < nh && p.status[gtid] == ST_RUNNING) {
     const int h = gtid;
-    const int ns = p.step_off[h + 1] - p.step_off[h];
+    const int ns = p.step_end[h] - p.step_beg[h];
     if (ns > 0) {
-      const int64_t gs = p.step_off[h];
+      const int64_t gs = p.step_beg[h];
       uint64_t live = 0;
       for (int64_t q = p.inv_off[gs]; q < p.inv_off[gs + 1]; ++q) {
         const int s = p.inv_slot[q];
@@ -283,19 +312,20 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
     const uint32_t pos = atomicAdd(&sFcount[0], 1u);
     if (pos < fcap) flist[((size_t)0 * nwg + wg) * fcap + pos] = e;
   }
-  if (!grid_sync(p, &sAbort)) goto done;
+  if (!grid_sync(p, &sAbort, nullptr, true)) goto done;
 
   {
     int phase = 0;
     for (int t = 0; t < p.max_t; ++t) {
       const int b = t & 1, nb = b ^ 1;
       // ============================================================ phase X
+      uint64_t ts = stamp();
       if (tid == 0) sFcount[nb] = 0;
       if (wg == 0 && tid == 0) st_agent(&p.running[(t + 2) & 3], 0u);
       if (gtid < nh) {
         const int h = gtid;
         int st = ld_agent(&p.status[h]);
-        const int ns = p.step_off[h + 1] - p.step_off[h];
+        const int ns = p.step_end[h] - p.step_beg[h];
         if (st == ST_RUNNING && t > 0 && ld_agent(&p.nonempty[(size_t)((t - 1) & 1) * nh + h]) == 0) {
           // no config survived RETURN t-1
           if (atomicCAS(&p.status[h], ST_RUNNING, ST_INVALID) == ST_RUNNING) p.fail_step[h] = t - 1;
@@ -307,7 +337,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
           } else {
             atomicAdd(&p.running[t & 3], 1u);
             // bring buffer nb (state of step t-1) to step t+1
-            const int64_t gs = p.step_off[h] + t;
+            const int64_t gs = p.step_beg[h] + t;
             uint64_t live = p.live[(size_t)nb * nh + h];
             if (t > 0) live &= ~(1ull << p.step_slot[gs - 1]);
             const int last = (t + 1 < ns) ? 1 : 0;
@@ -329,6 +359,8 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
         if (t > 0) st_agent(&p.nonempty[(size_t)((t - 1) & 1) * nh + h], 0u);
       }
       __syncthreads();
+      T[1] += stamp() - ts;
+      ts = stamp();
       {
         const uint32_t nf = min(sFcount[b], (uint32_t)fcap);
         const E* F = flist + ((size_t)b * nwg + wg) * fcap;
@@ -337,8 +369,8 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
           E e = F[i];
           const int h = hist_of(e.key);
           if (p.status[h] != ST_RUNNING) continue;
-          const int32_t so = p.step_off[h];
-          if (t >= p.step_off[h + 1] - so) continue;
+          const int32_t so = p.step_beg[h];
+          if (t >= p.step_end[h] - so) continue;
           const uint64_t bj = 1ull << p.step_slot[so + t];
           if (e.key & bj) {  // returned directly: only its post-return image matters
             E r = e;
@@ -351,13 +383,15 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
         if (tid == 0) sStat[SS_FIN] += nf;
         publish_counts(par, phase);
       }
-      if (!grid_sync(p, &sAbort)) goto done;
+      T[2] += stamp() - ts;
+      if (!grid_sync(p, &sAbort, &T[0], true)) goto done;  // publishes the slot tables
       ++phase;
       // ============================================================ levels
       for (;;) {
         const unsigned long long routed = ld_agent(&p.produced[(phase - 1) & 3]);
         if (routed == 0) break;
         const int pin = (phase - 1) & 1, pout = phase & 1;
+        ts = stamp();
         // prefix over the column of cells addressed to this workgroup
         if (tid < 64) {
           const int per = ((int)nwg + 63) / 64;
@@ -366,7 +400,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
           for (int q = 0; q < per; ++q) {
             const int s = tid * per + q;
             uint32_t c = 0;
-            if (s < (int)nwg) c = min(p.cell_cnt[((size_t)pin * nwg + wg) * nwg + s], (uint32_t)ccap);
+            if (s < (int)nwg) c = min(ld_agent(&p.cell_cnt[((size_t)pin * nwg + wg) * nwg + s]), (uint32_t)ccap);
             vals[q] = c;
             sum += c;
           }
@@ -384,19 +418,30 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
           if (tid == 63) sPref[nwg] = incl;
         }
         __syncthreads();
-        const uint32_t total = sPref[nwg];
+        T[3] += stamp() - ts;
+        ts = stamp();
+        const uint32_t in_cells = sPref[nwg];
+        const uint32_t in_ovf = (uint32_t)min((uint64_t)ld_agent(&p.ovf_cnt[(size_t)pin * nwg + wg]),
+                                              (uint64_t)p.ovf_cap);
+        const uint32_t total = in_cells + in_ovf;
         const E* col = cells + ((size_t)pin * nwg + wg) * nwg * ccap;
+        const E* ovf_in = (const E*)p.ovf + ((size_t)pin * nwg + wg) * p.ovf_cap;
         for (uint32_t i = tid; i < total; i += BLOCK) {
-          // source cell by binary search over the prefix
-          int lo = 0, hi = (int)nwg;  // sPref[lo] <= i < sPref[hi]
-          while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (sPref[mid] <= i) lo = mid; else hi = mid;
+          E e;
+          if (i < in_cells) {
+            // source cell by binary search over the prefix
+            int lo = 0, hi = (int)nwg;  // sPref[lo] <= i < sPref[hi]
+            while (hi - lo > 1) {
+              const int mid = (lo + hi) >> 1;
+              if (sPref[mid] <= i) lo = mid; else hi = mid;
+            }
+            e = get_entry(&col[(size_t)lo * ccap + (i - sPref[lo])]);
+          } else {
+            e = get_entry(&ovf_in[i - in_cells]);
           }
-          const E e = col[(size_t)lo * ccap + (i - sPref[lo])];
           const int h = hist_of(e.key);
           if (p.status[h] != ST_RUNNING) continue;
-          const int32_t so = p.step_off[h];
+          const int32_t so = p.step_beg[h];
           const uint64_t bj = 1ull << p.step_slot[so + t];
           E o = e;
           if (e.key & MARK) {
@@ -418,10 +463,16 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
             if (!(atomicOr(&sNE[h >> 5], bit) & bit)) st_agent(&p.nonempty[(size_t)b * nh + h], 1u);
           }
         }
+        __syncthreads();
+        if (tid == 0 && in_ovf) st_agent(&p.ovf_cnt[(size_t)pin * nwg + wg], 0u);
+        T[4] += stamp() - ts;
+        ts = stamp();
         publish_counts(pout, phase);
-        if (!grid_sync(p, &sAbort)) goto done;
+        T[5] += stamp() - ts;
+        if (!grid_sync(p, &sAbort, &T[0], false)) goto done;
         ++phase;
       }
+      ts = stamp();
       // ============================================================ end of step
       if (tid == 0) {
         sStat[SS_FOUT] += min(sFcount[nb], (uint32_t)fcap);
@@ -431,12 +482,18 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
       for (int i = tid; i < (1 << O_LOG); i += BLOCK) sO[i] = EMPTY;
       for (int i = tid; i < HMAX / 32; i += BLOCK) sNE[i] = 0;
       {
-        const uint32_t used = min(sSpillUsed, spill_limit);
-        for (uint32_t i = tid; i < used; i += BLOCK)
-          __hip_atomic_store(&spill[spill_pos[i]], EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t used = sSpillUsed;
+        if (used <= spill_limit) {
+          for (uint32_t i = tid; i < used; i += BLOCK)
+            __hip_atomic_store(&spill[spill_pos[i]], EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          for (uint32_t i = tid; i <= spill_mask; i += BLOCK)
+            __hip_atomic_store(&spill[i], EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
       __syncthreads();
       if (tid == 0) sSpillUsed = 0;
+      T[6] += stamp() - ts;
       if (ld_agent(&p.running[t & 3]) == 0) break;  // no history processed step t: all done
       __syncthreads();
     }
@@ -445,6 +502,8 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
 
 done:
   __syncthreads();
+  if (tid == 0 && p.stamps)
+    for (int i = 0; i < 8; ++i) p.stamps[(size_t)wg * 8 + i] = T[i];
   for (int h = tid; h < nh; h += BLOCK)
     if (sExpl[h]) atomicAdd(&p.explored[h], (unsigned long long)sExpl[h]);
   if (tid == 0) {

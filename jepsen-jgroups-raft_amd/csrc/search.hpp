@@ -29,10 +29,16 @@ struct CntEntry {  // counter config: key [hist | mask]; the value is a function
   int64_t st;
 };
 
+// Two-level arrival counters (8 groups of workgroups, then a top counter) and the release
+// generation, each on its own 128-B line.
 struct GridBar {
-  unsigned count;
   unsigned gen;
+  unsigned pad0[31];
+  unsigned top;
+  unsigned pad1[31];
+  unsigned grp[8][32];
 };
+constexpr int SENT_LOG = 11;  // LDS filter of candidates already routed this phase
 
 struct SearchParams {
   int32_t n_hist, nwg;
@@ -41,7 +47,8 @@ struct SearchParams {
   int32_t max_t;  // run steps t < max_t (failure-frontier dumps); INT32_MAX otherwise
   int32_t model;
   // read-only encoded history (see encode.hpp)
-  const int32_t* step_off;   // [n_hist+1]
+  const int32_t* step_beg;   // [n_hist] first global step of each history
+  const int32_t* step_end;   // [n_hist] one past its last step
   const uint8_t* step_slot;  // [total_steps]
   const int64_t* inv_off;    // [total_steps+1]
   const uint8_t* inv_slot;
@@ -63,6 +70,9 @@ struct SearchParams {
   uint32_t* fcount;    // [2][nwg] (written at exit)
   void* cells;         // [2][nwg dst][nwg src][cell_cap] candidate shuffle cells
   uint32_t* cell_cnt;  // [2][nwg dst][nwg src]
+  void* ovf;           // [2][nwg dst][ovf_cap] per-destination overflow of full cells
+  uint32_t* ovf_cnt;   // [2][nwg dst] (global atomic reservation; rare path)
+  int64_t ovf_cap;
   uint64_t* spill;     // [nwg][1 << spill_log] HBM overflow of the LDS tables
   uint32_t* spill_pos; // [nwg][1 << spill_log] used positions (for clearing)
   // grid sync and counters
@@ -71,6 +81,7 @@ struct SearchParams {
   unsigned* running;             // [4] histories active per step (step slot)
   int32_t* flags;                // [FL_N]
   unsigned long long* stats;     // [SS_N]
+  unsigned long long* stamps;    // [nwg][8] phase cycle stamps (debug; may be null)
 };
 
 // Host launcher (search.hip). Returns hipSuccess or the launch error.

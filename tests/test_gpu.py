@@ -229,3 +229,45 @@ def test_checker_api_counter_kats():
         c = checker.linearizable({"model": model.CounterModel(0), "algorithm": "linear"})
         r = c.check({}, kat["history"], {})
         assert r["valid?"] is kat["valid"], kat["name"]
+
+
+@pytest.mark.parametrize("path", ["keys", "grid"])
+def test_gpu_both_kernels_agree_with_oracle(path, monkeypatch):
+    """The per-history kernel (keys.hip) and the hash-partitioned grid kernel (search.hip)
+    must give identical answers on the same batch."""
+    monkeypatch.setenv("LC_PATH", path)
+    h = synth.gen_register_keys(40, 400, 5, 0.02, config_id=5, invalid_keys=(3, 17, 33))
+    g = _lib.check(1, 0, h)
+    exp = oracle.check_many("cas-register", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, path)
+    c = H.concat([synth.gen_counter(300, 5, 0.005, 7700 + t, invalid=(t % 4 == 0)) for t in range(20)])
+    gc = _lib.check(2, 0, c)
+    ec = oracle.check_many("counter", c)
+    for k in range(c.n_hist):
+        _cmp(gc, ec[k], k, path + "-counter")
+
+
+def test_gpu_keys_capacity_fallback(monkeypatch):
+    """Histories that outgrow a workgroup's scratch are re-run by the grid kernel."""
+    monkeypatch.setenv("LC_PATH", "keys")
+    monkeypatch.setenv("LC_KCAP", "64")
+    h = synth.gen_register_keys(32, 600, 5, 0.02, config_id=6, invalid_keys=(4,))
+    g = _lib.check(1, 0, h)
+    exp = oracle.check_many("cas-register", h)
+    assert max(e["max_frontier"] for e in exp) > 64  # the fallback really ran
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, "fallback")
+
+
+def test_gpu_cell_overflow_buckets(monkeypatch):
+    """Cells of 4 entries force most candidates through the per-destination overflow buckets,
+    and a 64-entry bucket forces a capacity regrow and re-run: answers must not change."""
+    monkeypatch.setenv("LC_PATH", "grid")
+    monkeypatch.setenv("LC_CELLCAP", "4")
+    monkeypatch.setenv("LC_OVFCAP", "64")
+    h = synth.gen_register_keys(12, 500, 5, 0.02, config_id=8, invalid_keys=(5,))
+    g = _lib.check(1, 0, h)
+    exp = oracle.check_many("cas-register", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, "overflow")
