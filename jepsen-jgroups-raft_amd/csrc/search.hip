@@ -140,6 +140,17 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
   const uint32_t spill_limit = (3u << p.spill_log) / 4;
 
   // ---------------------------------------------------------------- helpers
+  // slot operands: register -> one word (b << 32) | a; counter -> kind, a, d
+  auto set_op = [&](size_t oi, int64_t q) {
+    if constexpr (MODEL == 1) {
+      p.op_a[oi] = (int64_t)(((uint64_t)(uint32_t)(int32_t)p.inv_b[q] << 32) |
+                             (uint64_t)(uint32_t)(int32_t)p.inv_a[q]);
+    } else {
+      p.op_kind[oi] = p.inv_kind[q];
+      p.op_a[oi] = p.inv_a[q];
+      p.op_b[oi] = p.inv_b[q];
+    }
+  };
   auto hist_of = [&](uint64_t key) -> int { return (int)((key & ~MARK) >> p.hist_shift); };
 
   // spill: WG-private open-addressing table in HBM (workgroup-scope atomics; stays on this CU)
@@ -202,41 +213,65 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
   };
 
   // expand config e of history h at step t: linearize each live, not-yet-linearized slot
+  // expand config e of history h at step t: linearize each live, not-yet-linearized slot.
+  // Slot operands for up to 8 candidates are loaded together (independent loads in flight).
   auto expand = [&](const E& e, int h, int b, uint64_t bj, int par) -> uint32_t {
     const uint64_t key = e.key;
     const size_t hb = ((size_t)b * nh + h);
     uint64_t todo = p.live[hb] & ~(key & mmask);
     uint32_t n = 0;
+    constexpr int CH = 4;  // candidates whose operands load together
     while (todo) {
-      const int k = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const size_t oi = hb * 64 + k;
-      E ne;
-      if constexpr (MODEL == 1) {
-        // CASRegister.step [ext]: ok iff a = any or a = state; state := b unless keep
-        const int64_t a = p.op_a[oi], nb = p.op_b[oi];
-        const int64_t s = (int64_t)((key >> p.state_shift) & smask);
-        if (a != -1 && a != s) continue;
-        const uint64_t s2 = (uint64_t)(nb >= 0 ? nb : s);
-        ne.key = (key & ~(smask << p.state_shift)) | (s2 << p.state_shift) | (1ull << k);
-      } else {
-        // CounterModel.step (counter.clj:102-127): v +/- d, optional pre/post equality
-        const uint8_t kind = p.op_kind[oi];
-        const int64_t a = p.op_a[oi], d = p.op_b[oi];
-        const int64_t st = e.st;
-        int64_t r;
-        bool ovf = (kind & 4) ? __builtin_sub_overflow(st, d, &r) : __builtin_add_overflow(st, d, &r);
-        if (ovf) {  // Clojure +/- throw -> the checker errors -> :valid? :unknown
-          atomicCAS(&p.status[h], ST_RUNNING, ST_MODEL);
-          continue;
-        }
-        if ((kind & 1) && st != a) continue;
-        if ((kind & 2) && r != a) continue;
-        ne.key = key | (1ull << k);
-        ne.st = r;
+      int ks[CH];
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        ks[q] = todo ? __builtin_ctzll(todo) : -1;
+        todo &= todo - 1;
       }
-      route(ne, ne.key & ~bj, par);
-      ++n;
+      int64_t oa[CH], ob[CH];
+      uint8_t okd[CH];
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        if (ks[q] < 0) continue;
+        const size_t oi = hb * 64 + ks[q];
+        oa[q] = p.op_a[oi];
+        if constexpr (MODEL == 2) {
+          ob[q] = p.op_b[oi];
+          okd[q] = p.op_kind[oi];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        const int k = ks[q];
+        if (k < 0) continue;
+        E ne;
+        if constexpr (MODEL == 1) {
+          // CASRegister.step [ext]: ok iff a = any or a = state; state := b unless keep.
+          // operands packed as (b << 32) | a (int32 each)
+          const int64_t a = (int32_t)(uint32_t)oa[q], nb = (int32_t)(uint32_t)((uint64_t)oa[q] >> 32);
+          const int64_t s = (int64_t)((key >> p.state_shift) & smask);
+          if (a != -1 && a != s) continue;
+          const uint64_t s2 = (uint64_t)(nb >= 0 ? nb : s);
+          ne.key = (key & ~(smask << p.state_shift)) | (s2 << p.state_shift) | (1ull << k);
+        } else {
+          // CounterModel.step (counter.clj:102-127): v +/- d, optional pre/post equality
+          const uint8_t kind = okd[q];
+          const int64_t a = oa[q], d = ob[q];
+          const int64_t st = e.st;
+          int64_t r;
+          bool ovf = (kind & 4) ? __builtin_sub_overflow(st, d, &r) : __builtin_add_overflow(st, d, &r);
+          if (ovf) {  // Clojure +/- throw -> the checker errors -> :valid? :unknown
+            atomicCAS(&p.status[h], ST_RUNNING, ST_MODEL);
+            continue;
+          }
+          if ((kind & 1) && st != a) continue;
+          if ((kind & 2) && r != a) continue;
+          ne.key = key | (1ull << k);
+          ne.st = r;
+        }
+        route(ne, ne.key & ~bj, par);
+        ++n;
+      }
     }
     return n;
   };
@@ -291,9 +326,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
       for (int64_t q = p.inv_off[gs]; q < p.inv_off[gs + 1]; ++q) {
         const int s = p.inv_slot[q];
         const size_t oi = ((size_t)0 * nh + h) * 64 + s;
-        p.op_kind[oi] = p.inv_kind[q];
-        p.op_a[oi] = p.inv_a[q];
-        p.op_b[oi] = p.inv_b[q];
+        set_op(oi, q);
         live |= 1ull << s;
       }
       p.live[h] = live;
@@ -347,9 +380,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
               for (int64_t q = p.inv_off[g2]; q < p.inv_off[g2 + 1]; ++q) {
                 const int s = p.inv_slot[q];
                 const size_t oi = ((size_t)nb * nh + h) * 64 + s;
-                p.op_kind[oi] = p.inv_kind[q];
-                p.op_a[oi] = p.inv_a[q];
-                p.op_b[oi] = p.inv_b[q];
+                set_op(oi, q);
                 live |= 1ull << s;
               }
             }
@@ -426,41 +457,54 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
         const uint32_t total = in_cells + in_ovf;
         const E* col = cells + ((size_t)pin * nwg + wg) * nwg * ccap;
         const E* ovf_in = (const E*)p.ovf + ((size_t)pin * nwg + wg) * p.ovf_cap;
-        for (uint32_t i = tid; i < total; i += BLOCK) {
-          E e;
-          if (i < in_cells) {
-            // source cell by binary search over the prefix
-            int lo = 0, hi = (int)nwg;  // sPref[lo] <= i < sPref[hi]
-            while (hi - lo > 1) {
-              const int mid = (lo + hi) >> 1;
-              if (sPref[mid] <= i) lo = mid; else hi = mid;
+        // each thread fetches R entries before touching any (R sc1 loads in flight)
+        constexpr int R = MODEL == 1 ? 4 : 2;
+        for (uint32_t base = 0; base < total; base += BLOCK * R) {
+          E ent[R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const uint32_t i = base + r * BLOCK + tid;
+            ent[r].key = EMPTY;
+            if (i >= total) continue;
+            if (i < in_cells) {
+              // source cell by binary search over the prefix
+              int lo = 0, hi = (int)nwg;  // sPref[lo] <= i < sPref[hi]
+              while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (sPref[mid] <= i) lo = mid; else hi = mid;
+              }
+              ent[r] = get_entry(&col[(size_t)lo * ccap + (i - sPref[lo])]);
+            } else {
+              ent[r] = get_entry(&ovf_in[i - in_cells]);
             }
-            e = get_entry(&col[(size_t)lo * ccap + (i - sPref[lo])]);
-          } else {
-            e = get_entry(&ovf_in[i - in_cells]);
           }
-          const int h = hist_of(e.key);
-          if (p.status[h] != ST_RUNNING) continue;
-          const int32_t so = p.step_beg[h];
-          const uint64_t bj = 1ull << p.step_slot[so + t];
-          E o = e;
-          if (e.key & MARK) {
-            o.key = e.key & ~MARK;
-          } else {
-            if (!lds_insert(sS, S_LOG, e.key, 0)) continue;  // seen in this closure
-            atomicAdd(&sExpl[h], 1u);
-            if (!(e.key & bj)) {  // returning op not linearized yet: keep exploring
-              expand(e, h, b, bj, pout);
-              continue;
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const E e = ent[r];
+            if (e.key == EMPTY) continue;
+            const int h = hist_of(e.key);
+            if (p.status[h] != ST_RUNNING) continue;
+            const int32_t so = p.step_beg[h];
+            const uint64_t bj = 1ull << p.step_slot[so + t];
+            E o = e;
+            if (e.key & MARK) {
+              o.key = e.key & ~MARK;
+            } else {
+              if (!lds_insert(sS, S_LOG, e.key, 0)) continue;  // seen in this closure
+              atomicAdd(&sExpl[h], 1u);
+              if (!(e.key & bj)) {  // returning op not linearized yet: keep exploring
+                expand(e, h, b, bj, pout);
+                continue;
+              }
+              o.key = e.key & ~bj;  // linearized: return it
             }
-            o.key = e.key & ~bj;  // linearized: return it
-          }
-          if (lds_insert(sO, O_LOG, o.key, MARK)) {
-            const uint32_t pos = atomicAdd(&sFcount[nb], 1u);
-            if (pos < fcap) flist[((size_t)nb * nwg + wg) * fcap + pos] = o;
-            else __hip_atomic_store(&p.flags[FL_OVERFLOW], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t bit = 1u << (h & 31);
-            if (!(atomicOr(&sNE[h >> 5], bit) & bit)) st_agent(&p.nonempty[(size_t)b * nh + h], 1u);
+            if (lds_insert(sO, O_LOG, o.key, MARK)) {
+              const uint32_t pos = atomicAdd(&sFcount[nb], 1u);
+              if (pos < fcap) flist[((size_t)nb * nwg + wg) * fcap + pos] = o;
+              else __hip_atomic_store(&p.flags[FL_OVERFLOW], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const uint32_t bit = 1u << (h & 31);
+              if (!(atomicOr(&sNE[h >> 5], bit) & bit)) st_agent(&p.nonempty[(size_t)b * nh + h], 1u);
+            }
           }
         }
         __syncthreads();
