@@ -130,8 +130,9 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  *  6 frontier configs written                             7 closure configs inserted
  *  8 config bytes (C)                                     9 algorithmic bytes
  * 10 workgroups                                          11 spill inserts
+ * 12 histories decided by the dense closure-table kernels 13 dense kernels' ms (part of 0)
  */
-#define LC_STATS_N 12
+#define LC_STATS_N 14
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
 void lc_plan_destroy(lc_plan* p);
 

@@ -22,6 +22,7 @@
 
 #include "../../include/lincheck.h"
 #include "bounds.hpp"
+#include "dense.hpp"
 #include "encode.hpp"
 #include "keys.hpp"
 #include "search.hpp"
@@ -105,7 +106,7 @@ struct lc_plan {
     int mask_bits, state_bits, hist_bits;
   };
   std::vector<Batch> batches;
-  int path = 0;  // 0 auto, 1 keys kernel first, 2 grid kernel only
+  int path = 0;  // 0 auto (dense tables, then grid), 1 keys kernel first, 2 grid kernel only
   int nwg = 0, cell_cap = 256, f_cap = 65536, spill_log = 17;
   int64_t ovf_cap = 1 << 18;
   int knwg = 0;
@@ -124,6 +125,13 @@ struct lc_plan {
   DevArray d_bar, d_produced, d_running, d_flags, d_stats, d_stamps;
   // keys-kernel per-workgroup storage
   DevArray d_kscratch, d_kspill, d_kspillpos, d_kstatus, d_kfail, d_kexplored;
+  // dense closure tables (narrow cas-register histories; dense.hpp)
+  std::vector<int> dense_b, dense_w;  // block-team / wave-team histories, heaviest first
+  DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
+  int64_t dstream_words = 0;
+  int dgrid_b = 0, dgrid_w = 0;
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool spill_clean = false, kspill_clean = false;
   // results
   std::vector<int32_t> status, fail_step;
@@ -138,6 +146,9 @@ struct lc_plan {
   ~lc_plan() {
     if (ev0) hipEventDestroy(ev0);
     if (ev1) hipEventDestroy(ev1);
+    if (ev_fork) hipEventDestroy(ev_fork);
+    if (ev_join) hipEventDestroy(ev_join);
+    if (stream2) hipStreamDestroy(stream2);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -186,7 +197,12 @@ struct lc_plan {
     if (!stream) HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     if (!ev0) HIP_TRY(hipEventCreate(&ev0));
     if (!ev1) HIP_TRY(hipEventCreate(&ev1));
+    if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    if (!ev_fork) HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    if (!ev_join) HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     nwg = search_grid_size(model);
+    dgrid_b = dense_grid_size(false);
+    dgrid_w = dense_grid_size(true);
     knwg = keys_grid_size(model);
     if (nwg <= 0 || knwg <= 0) {
       last_error = "search kernels cannot be resident (occupancy 0)";
@@ -195,6 +211,7 @@ struct lc_plan {
     const char* e = getenv("LC_PATH");
     if (e && !strcmp(e, "keys")) path = 1;
     if (e && !strcmp(e, "grid")) path = 2;
+    if (e && !strcmp(e, "dense")) path = 0;
     // test hooks: shrink the keys kernel's per-workgroup capacities to force the fallback
     if ((e = getenv("LC_KCAP")) && atoll(e) > 0) kfcap = klcap = atoll(e);
     // test hooks: tiny cells / overflow buckets exercise the overflow and regrow paths
@@ -236,6 +253,128 @@ struct lc_plan {
     if ((rc = upload(d_kbits, kbi))) return rc;
     if ((rc = upload(d_order, order))) return rc;
     HIP_TRY(d_queue.ensure(8));
+    return build_dense();
+  }
+
+  // Step streams for the dense closure-table kernels (format: dense.hpp). Eligible:
+  // cas-register, <= DENSE_MAX_STATES register values, live width <= DENSE_LMAX.
+  int build_dense() {
+    dense_b.clear();
+    dense_w.clear();
+    if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0) return 0;
+    const int n = enc.n_hist;
+    std::vector<uint32_t> words;
+    std::vector<int64_t> sbeg(n, 0);
+    std::vector<int32_t> nst(n, 0);
+    std::vector<int8_t> lm(n, 0);
+    std::vector<double> cost(n, 0.0);
+    for (int h = 0; h < n; ++h) {
+      if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || enc.live_max[h] > DENSE_LMAX) continue;
+      sbeg[h] = (int64_t)words.size();
+      nst[h] = enc.n_steps(h);
+      lm[h] = (int8_t)std::max(1, enc.live_max[h]);
+      uint32_t live = 0;
+      for (int t = 0; t < nst[h]; ++t) {
+        const int64_t g = (int64_t)enc.step_off[h] + t;
+        if (t > 0) live &= ~(1u << enc.step_slot[g - 1]);
+        const int64_t q0 = enc.inv_off[g], q1 = enc.inv_off[g + 1];
+        for (int64_t q = q0; q < q1; ++q) live |= 1u << enc.inv_slot[q];
+        const uint32_t j = enc.step_slot[g];
+        words.push_back(live | (j << 22) | ((uint32_t)(q1 - q0) << 27));
+        for (int64_t q = q0; q < q1; ++q) {
+          const int64_t a = enc.inv_a[q], b = enc.inv_b[q];
+          const uint32_t am = a == R_ANY ? 0xffu : (a == R_NEVER ? 0u : (1u << a));
+          const uint32_t bm = b < 0 ? 0u : (1u << b);
+          words.push_back((uint32_t)enc.inv_slot[q] | (am << 8) | (bm << 16));
+        }
+        const int L = 32 - __builtin_clz(live);
+        cost[h] += (double)(1u << L) * L;
+      }
+      (enc.live_max[h] <= DENSE_WAVE_LMAX ? dense_w : dense_b).push_back(h);
+    }
+    auto heavy_first = [&](int a, int b) { return cost[a] > cost[b]; };
+    std::stable_sort(dense_b.begin(), dense_b.end(), heavy_first);
+    std::stable_sort(dense_w.begin(), dense_w.end(), heavy_first);
+    std::vector<int32_t> ord(dense_b.begin(), dense_b.end());
+    ord.insert(ord.end(), dense_w.begin(), dense_w.end());
+    dstream_words = (int64_t)words.size();
+    int rc;
+    if ((rc = upload(d_dstream, words))) return rc;
+    if ((rc = upload(d_dsbeg, sbeg))) return rc;
+    if ((rc = upload(d_dnsteps, nst))) return rc;
+    if ((rc = upload(d_dlmax, lm))) return rc;
+    if ((rc = upload(d_dorder, ord))) return rc;
+    HIP_TRY(d_dqueue.ensure(8));
+    HIP_TRY(d_dstatus.ensure((size_t)std::max(n, 1) * 4));
+    HIP_TRY(d_dfail.ensure((size_t)std::max(n, 1) * 4));
+    HIP_TRY(d_dexpl.ensure((size_t)std::max(n, 1) * 8));
+    return 0;
+  }
+
+  // dense closure-table kernels: block teams on one stream, wave teams beside them on a
+  // second stream (they fill the CUs the wide histories release)
+  int run_dense(float* ms) {
+    const int nb = (int)dense_b.size(), nw = (int)dense_w.size();
+    if (nb + nw == 0) return 0;
+    const int n = enc.n_hist;
+    HIP_TRY(d_stats.ensure(SS_N * 8));
+    HIP_TRY(hipMemsetAsync(d_dqueue.p, 0, 8, stream));
+    HIP_TRY(hipMemsetAsync(d_stats.p, 0, SS_N * 8, stream));
+    DenseParams p{};
+    p.sbeg = d_dsbeg.as<int64_t>();
+    p.nsteps = d_dnsteps.as<int32_t>();
+    p.lmax = d_dlmax.as<int8_t>();
+    p.stream = d_dstream.as<uint32_t>();
+    p.stream_words = dstream_words;
+    p.status = d_dstatus.as<int32_t>();
+    p.fail_step = d_dfail.as<int32_t>();
+    p.explored = d_dexpl.as<unsigned long long>();
+    p.stats = d_stats.as<unsigned long long>();
+    HIP_TRY(hipEventRecord(ev0, stream));
+    if (nw) {
+      HIP_TRY(hipEventRecord(ev_fork, stream));
+      HIP_TRY(hipStreamWaitEvent(stream2, ev_fork, 0));
+      DenseParams q = p;
+      q.n = nw;
+      q.order = d_dorder.as<int32_t>() + nb;
+      q.queue = d_dqueue.as<int32_t>() + 1;
+      const int grid = std::min(dgrid_w, (nw + 15) / 16);
+      HIP_TRY(launch_dense(q, true, grid, stream2));
+      HIP_TRY(hipEventRecord(ev_join, stream2));
+    }
+    if (nb) {
+      DenseParams q = p;
+      q.n = nb;
+      q.order = d_dorder.as<int32_t>();
+      q.queue = d_dqueue.as<int32_t>();
+      HIP_TRY(launch_dense(q, false, std::min(dgrid_b, nb), stream));
+    }
+    if (nw) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
+    HIP_TRY(hipEventRecord(ev1, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
+    *ms += t;
+    std::vector<int32_t> st(n), fs(n);
+    std::vector<unsigned long long> ex(n);
+    HIP_TRY(hipMemcpy(st.data(), d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(fs.data(), d_dfail.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(ex.data(), d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost));
+    unsigned long long ss[SS_N];
+    HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
+    for (int h : dense_b) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
+    for (int h : dense_w) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
+    stats[1] += (nb ? 1 : 0) + (nw ? 1 : 0);
+    stats[12] += nb + nw;
+    stats[13] += t;
+    stats[2] += (double)ss[SS_STEPS];
+    stats[4] += (double)ss[SS_FOUT] + (nb + nw);  // frontier in = previous frontier out (+ initial)
+    stats[5] += (double)ss[SS_CAND];
+    stats[6] += (double)ss[SS_FOUT];
+    if (debug())
+      fprintf(stderr, "[lincheck] dense: %d block-team + %d wave-team histories (grids %d/%d): %.3f ms, "
+              "steps=%llu cand=%llu Fout=%llu\n", nb, nw, std::min(dgrid_b, nb), std::min(dgrid_w, (nw + 15) / 16), t,
+              ss[SS_STEPS], ss[SS_CAND], ss[SS_FOUT]);
     return 0;
   }
 
@@ -555,6 +694,14 @@ struct lc_plan {
     int rc = 0;
     std::vector<int> grid_ids;
     const bool keys = max_t == INT32_MAX && path == 1;
+    const bool dense = max_t == INT32_MAX && path == 0 && (dense_b.size() + dense_w.size()) > 0;
+    std::vector<char> done(enc.n_hist, 0);
+    if (dense) {
+      rc = run_dense(&ms);
+      if (rc) return rc;
+      for (int h : dense_b) done[h] = 1;
+      for (int h : dense_w) done[h] = 1;
+    }
     if (keys) {
       rc = run_keys(&ms);
       if (rc) return rc;
@@ -562,7 +709,7 @@ struct lc_plan {
         if (status[h] == ST_CAPACITY) grid_ids.push_back(h);
     } else {
       for (int h = 0; h < enc.n_hist; ++h)
-        if (!enc.err[h]) grid_ids.push_back(h);
+        if (!enc.err[h] && !done[h]) grid_ids.push_back(h);
     }
     if (!grid_ids.empty()) {
       rc = run_grid(grid_ids, &ms);

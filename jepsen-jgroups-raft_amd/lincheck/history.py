@@ -164,9 +164,12 @@ def subhistories(ops: Iterable[Dict[str, Any]]) -> History:
 def concat(hs: Sequence[History]) -> History:
     if not hs:
         return from_columns([], [], [], [], [], [], [], off=[0])
-    lens = [h.n for h in hs]
-    off = np.zeros(len(hs) + 1, np.int64)
-    off[1:] = np.cumsum(lens)
+    # every input keeps its own sub-histories
+    offs, base = [np.zeros(1, np.int64)], 0
+    for h in hs:
+        offs.append(np.asarray(h.off[1:], np.int64) - int(h.off[0]) + base)
+        base += h.n
+    off = np.concatenate(offs)
     keys = None
     if all(h.keys is not None for h in hs):
         keys = [k for h in hs for k in h.keys]

@@ -231,10 +231,85 @@ def test_checker_api_counter_kats():
         assert r["valid?"] is kat["valid"], kat["name"]
 
 
-@pytest.mark.parametrize("path", ["keys", "grid"])
+def _live_width(h, k):
+    """Widest live-slot window (lowest-free-first slots, crashed ops keep theirs) of history k:
+    the table width the dense kernel needs."""
+    a, b = int(h.off[k]), int(h.off[k + 1])
+    comp, pend = {}, {}
+    for i in range(a, b):
+        p = int(h.process[i])
+        if h.type[i] == 0:
+            pend[p] = i
+        else:
+            comp[pend.pop(p)] = int(h.type[i])
+    used, slot, width = set(), {}, 0
+    for i in range(a, b):
+        p = int(h.process[i])
+        if h.type[i] == 0:
+            if comp.get(i) == 2:
+                continue
+            s = 0
+            while s in used:
+                s += 1
+            used.add(s)
+            slot[p] = s
+            width = max(width, max(used) + 1)
+        elif h.type[i] == 1:
+            used.discard(slot.pop(p))
+        elif h.type[i] == 3:
+            slot.pop(p, None)
+    return width
+
+
+def test_gpu_dense_tables_vs_oracle():
+    """Dense closure tables (dense.hip): wave teams (width <= 12), workgroup teams (13..17)
+    and the wide histories routed to the grid kernel, in one batch, bit-exact with the oracle."""
+    hs = [synth.gen_register_keys(28, 1000, 5, 0.01, config_id=3, invalid_keys=(2, 9, 20))]
+    hs += [synth.gen_register(150, 5, 0.12, 31000 + t, invalid=(t % 2 == 0)) for t in range(6)]
+    h = H.concat(hs)
+    widths = [_live_width(h, k) for k in range(h.n_hist)]
+    assert min(widths) <= 12 and any(13 <= w <= 17 for w in widths) and max(widths) > 17
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    g = p.results()
+    s = p.stats()
+    assert s["dense_histories"] == sum(w <= 17 for w in widths)
+    exp = oracle.check_many("cas-register", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"dense w={widths[k]}")
+    assert any(e["valid"] == 0 for e in exp)
+    p.close()
+
+
+def test_gpu_dense_edge_histories():
+    """Empty, single-op, read-only, all-crashed and fail-only histories through the dense path."""
+    ops = [
+        [],
+        [{"process": 0, "type": "invoke", "f": "read", "value": None},
+         {"process": 0, "type": "ok", "f": "read", "value": None}],
+        [{"process": 0, "type": "invoke", "f": "read", "value": None},
+         {"process": 0, "type": "ok", "f": "read", "value": 3}],
+        [{"process": 0, "type": "invoke", "f": "write", "value": 1},
+         {"process": 0, "type": "info", "f": "write", "value": 1},
+         {"process": 1, "type": "invoke", "f": "cas", "value": [1, 2]},
+         {"process": 1, "type": "info", "f": "cas", "value": [1, 2]},
+         {"process": 2, "type": "invoke", "f": "read", "value": None},
+         {"process": 2, "type": "ok", "f": "read", "value": 2}],
+        [{"process": 0, "type": "invoke", "f": "cas", "value": [0, 1]},
+         {"process": 0, "type": "fail", "f": "cas", "value": [0, 1]}],
+    ]
+    h = H.concat([H.encode(o) for o in ops])
+    g = _lib.check(1, 0, h)
+    exp = oracle.check_many("cas-register", h, n_threads=2)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"edge{k}")
+    assert [int(v) for v in g["valid"]] == [1, 1, 0, 1, 1]
+
+
+@pytest.mark.parametrize("path", ["keys", "grid", "dense"])
 def test_gpu_both_kernels_agree_with_oracle(path, monkeypatch):
-    """The per-history kernel (keys.hip) and the hash-partitioned grid kernel (search.hip)
-    must give identical answers on the same batch."""
+    """The per-history kernel (keys.hip), the hash-partitioned grid kernel (search.hip) and
+    the dense closure tables (dense.hip) must give identical answers on the same batch."""
     monkeypatch.setenv("LC_PATH", path)
     h = synth.gen_register_keys(40, 400, 5, 0.02, config_id=5, invalid_keys=(3, 17, 33))
     g = _lib.check(1, 0, h)
