@@ -126,12 +126,14 @@ struct lc_plan {
   // keys-kernel per-workgroup storage
   DevArray d_kscratch, d_kspill, d_kspillpos, d_kstatus, d_kfail, d_kexplored;
   // dense closure tables (narrow cas-register histories; dense.hpp)
-  std::vector<int> dense_b, dense_w;  // block-team / wave-team histories, heaviest first
-  DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
+  std::vector<int> dense_b, dense_w, dense_x;  // block / wave / wide teams, heaviest first
+  DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dwords, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
+  DevArray d_dstamps, d_gtab, d_ctl, d_abort;
   int64_t dstream_words = 0;
-  int dgrid_b = 0, dgrid_w = 0;
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int dgrid_b = 0, dgrid_w = 0, dgrid_x = 0;
+  int wide_g = 8, wide_teams = 8, dense_maxw = DENSE_WIDE_LMAX;  // LC_WIDE_G / LC_WIDE_TEAMS / LC_DENSE_MAXW
+  hipStream_t stream2 = nullptr, stream3 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
   bool spill_clean = false, kspill_clean = false;
   // results
   std::vector<int32_t> status, fail_step;
@@ -148,7 +150,9 @@ struct lc_plan {
     if (ev1) hipEventDestroy(ev1);
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_join) hipEventDestroy(ev_join);
+    if (ev_join2) hipEventDestroy(ev_join2);
     if (stream2) hipStreamDestroy(stream2);
+    if (stream3) hipStreamDestroy(stream3);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -200,9 +204,12 @@ struct lc_plan {
     if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
     if (!ev_fork) HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     if (!ev_join) HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    if (!stream3) HIP_TRY(hipStreamCreateWithFlags(&stream3, hipStreamNonBlocking));
+    if (!ev_join2) HIP_TRY(hipEventCreateWithFlags(&ev_join2, hipEventDisableTiming));
     nwg = search_grid_size(model);
-    dgrid_b = dense_grid_size(false);
-    dgrid_w = dense_grid_size(true);
+    dgrid_b = dense_grid_size(DENSE_BLOCK);
+    dgrid_w = dense_grid_size(DENSE_WAVE);
+    dgrid_x = dense_grid_size(DENSE_WIDE);
     knwg = keys_grid_size(model);
     if (nwg <= 0 || knwg <= 0) {
       last_error = "search kernels cannot be resident (occupancy 0)";
@@ -212,6 +219,10 @@ struct lc_plan {
     if (e && !strcmp(e, "keys")) path = 1;
     if (e && !strcmp(e, "grid")) path = 2;
     if (e && !strcmp(e, "dense")) path = 0;
+    // dense-path knobs (tests): wide-team size and count, widest history the tables take
+    if ((e = getenv("LC_WIDE_G")) && atoi(e) > 0) wide_g = atoi(e);
+    if ((e = getenv("LC_WIDE_TEAMS")) && atoi(e) > 0) wide_teams = atoi(e);
+    if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
     // test hooks: shrink the keys kernel's per-workgroup capacities to force the fallback
     if ((e = getenv("LC_KCAP")) && atoll(e) > 0) kfcap = klcap = atoll(e);
     // test hooks: tiny cells / overflow buckets exercise the overflow and regrow paths
@@ -257,11 +268,12 @@ struct lc_plan {
   }
 
   // Step streams for the dense closure-table kernels (format: dense.hpp). Eligible:
-  // cas-register, <= DENSE_MAX_STATES register values, live width <= DENSE_LMAX.
+  // cas-register, <= DENSE_MAX_STATES register values, live width <= dense_maxw.
   int build_dense() {
     dense_b.clear();
     dense_w.clear();
-    if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0) return 0;
+    dense_x.clear();
+    if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0 || dgrid_x <= 0) return 0;
     const int n = enc.n_hist;
     std::vector<uint32_t> words;
     std::vector<int64_t> sbeg(n, 0);
@@ -269,7 +281,7 @@ struct lc_plan {
     std::vector<int8_t> lm(n, 0);
     std::vector<double> cost(n, 0.0);
     for (int h = 0; h < n; ++h) {
-      if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || enc.live_max[h] > DENSE_LMAX) continue;
+      if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || enc.live_max[h] > dense_maxw) continue;
       sbeg[h] = (int64_t)words.size();
       nst[h] = enc.n_steps(h);
       lm[h] = (int8_t)std::max(1, enc.live_max[h]);
@@ -290,56 +302,95 @@ struct lc_plan {
         const int L = 32 - __builtin_clz(live);
         cost[h] += (double)(1u << L) * L;
       }
-      (enc.live_max[h] <= DENSE_WAVE_LMAX ? dense_w : dense_b).push_back(h);
+      const int lw = enc.live_max[h];
+      (lw <= DENSE_WAVE_LMAX ? dense_w : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
     }
     auto heavy_first = [&](int a, int b) { return cost[a] > cost[b]; };
     std::stable_sort(dense_b.begin(), dense_b.end(), heavy_first);
     std::stable_sort(dense_w.begin(), dense_w.end(), heavy_first);
+    std::stable_sort(dense_x.begin(), dense_x.end(), heavy_first);
     std::vector<int32_t> ord(dense_b.begin(), dense_b.end());
     ord.insert(ord.end(), dense_w.begin(), dense_w.end());
+    ord.insert(ord.end(), dense_x.begin(), dense_x.end());
     dstream_words = (int64_t)words.size();
     int rc;
     if ((rc = upload(d_dstream, words))) return rc;
     if ((rc = upload(d_dsbeg, sbeg))) return rc;
     if ((rc = upload(d_dnsteps, nst))) return rc;
     if ((rc = upload(d_dlmax, lm))) return rc;
+    if (!d_dwords.p) {
+      std::vector<uint32_t> wl(1u << DENSE_WORD_BITS);
+      dense_word_list(DENSE_WORD_BITS, wl.data());
+      if ((rc = upload(d_dwords, wl))) return rc;
+    }
     if ((rc = upload(d_dorder, ord))) return rc;
-    HIP_TRY(d_dqueue.ensure(8));
+    HIP_TRY(d_dqueue.ensure(16));
     HIP_TRY(d_dstatus.ensure((size_t)std::max(n, 1) * 4));
     HIP_TRY(d_dfail.ensure((size_t)std::max(n, 1) * 4));
     HIP_TRY(d_dexpl.ensure((size_t)std::max(n, 1) * 8));
     return 0;
   }
 
-  // dense closure-table kernels: block teams on one stream, wave teams beside them on a
-  // second stream (they fill the CUs the wide histories release)
+  // Dense closure-table kernels on three streams: wide teams first (every workgroup of a
+  // team must be resident), block teams beside them, wave teams filling the room the
+  // block teams leave on each CU.
   int run_dense(float* ms) {
-    const int nb = (int)dense_b.size(), nw = (int)dense_w.size();
-    if (nb + nw == 0) return 0;
+    const int nb = (int)dense_b.size(), nw = (int)dense_w.size(), nx = (int)dense_x.size();
+    if (nb + nw + nx == 0) return 0;
     const int n = enc.n_hist;
     HIP_TRY(d_stats.ensure(SS_N * 8));
-    HIP_TRY(hipMemsetAsync(d_dqueue.p, 0, 8, stream));
+    HIP_TRY(hipMemsetAsync(d_dqueue.p, 0, 16, stream));
     HIP_TRY(hipMemsetAsync(d_stats.p, 0, SS_N * 8, stream));
+    HIP_TRY(hipMemsetAsync(d_dexpl.p, 0, (size_t)std::max(n, 1) * 8, stream));
     DenseParams p{};
     p.sbeg = d_dsbeg.as<int64_t>();
     p.nsteps = d_dnsteps.as<int32_t>();
     p.lmax = d_dlmax.as<int8_t>();
+    p.words = d_dwords.as<uint32_t>();
     p.stream = d_dstream.as<uint32_t>();
     p.stream_words = dstream_words;
     p.status = d_dstatus.as<int32_t>();
     p.fail_step = d_dfail.as<int32_t>();
     p.explored = d_dexpl.as<unsigned long long>();
     p.stats = d_stats.as<unsigned long long>();
+    p.stamps = nullptr;
+    if (debug()) {
+      HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 16));
+      HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 16, stream));
+      p.stamps = d_dstamps.as<unsigned long long>();
+    }
+    const int G = std::max(1, std::min(wide_g, dgrid_x));
+    int teams = 0;
+    if (nx) {
+      teams = std::max(1, std::min(std::min(nx, wide_teams), dgrid_x / G));
+      HIP_TRY(d_gtab.ensure(((size_t)teams << DENSE_WORD_BITS) * 8));
+      HIP_TRY(d_ctl.ensure((size_t)teams * dense_ctl_bytes()));
+      HIP_TRY(d_abort.ensure(16));
+      HIP_TRY(hipMemsetAsync(d_ctl.p, 0, (size_t)teams * dense_ctl_bytes(), stream));
+      HIP_TRY(hipMemsetAsync(d_abort.p, 0, 16, stream));
+      p.team_size = G;
+      p.gtab = d_gtab.as<uint64_t>();
+      p.ctl = d_ctl.p;
+      p.abort = d_abort.as<int32_t>();
+    }
     HIP_TRY(hipEventRecord(ev0, stream));
+    HIP_TRY(hipEventRecord(ev_fork, stream));
+    if (nx) {
+      HIP_TRY(hipStreamWaitEvent(stream3, ev_fork, 0));
+      DenseParams q = p;
+      q.n = nx;
+      q.order = d_dorder.as<int32_t>() + nb + nw;
+      q.queue = d_dqueue.as<int32_t>() + 2;
+      HIP_TRY(launch_dense(q, DENSE_WIDE, teams * G, stream3));
+      HIP_TRY(hipEventRecord(ev_join2, stream3));
+    }
     if (nw) {
-      HIP_TRY(hipEventRecord(ev_fork, stream));
       HIP_TRY(hipStreamWaitEvent(stream2, ev_fork, 0));
       DenseParams q = p;
       q.n = nw;
       q.order = d_dorder.as<int32_t>() + nb;
       q.queue = d_dqueue.as<int32_t>() + 1;
-      const int grid = std::min(dgrid_w, (nw + 15) / 16);
-      HIP_TRY(launch_dense(q, true, grid, stream2));
+      HIP_TRY(launch_dense(q, DENSE_WAVE, std::min(dgrid_w, (nw + 3) / 4), stream2));
       HIP_TRY(hipEventRecord(ev_join, stream2));
     }
     if (nb) {
@@ -347,14 +398,23 @@ struct lc_plan {
       q.n = nb;
       q.order = d_dorder.as<int32_t>();
       q.queue = d_dqueue.as<int32_t>();
-      HIP_TRY(launch_dense(q, false, std::min(dgrid_b, nb), stream));
+      HIP_TRY(launch_dense(q, DENSE_BLOCK, std::min(dgrid_b, nb), stream));
     }
     if (nw) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
+    if (nx) HIP_TRY(hipStreamWaitEvent(stream, ev_join2, 0));
     HIP_TRY(hipEventRecord(ev1, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     float t = 0;
     HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
     *ms += t;
+    if (nx) {
+      int32_t ab = 0;
+      HIP_TRY(hipMemcpy(&ab, d_abort.p, 4, hipMemcpyDeviceToHost));
+      if (ab) {
+        last_error = "dense wide-team barrier watchdog fired (a team workgroup was not resident)";
+        return LC_E_INTERNAL;
+      }
+    }
     std::vector<int32_t> st(n), fs(n);
     std::vector<unsigned long long> ex(n);
     HIP_TRY(hipMemcpy(st.data(), d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost));
@@ -362,20 +422,59 @@ struct lc_plan {
     HIP_TRY(hipMemcpy(ex.data(), d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost));
     unsigned long long ss[SS_N];
     HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
-    for (int h : dense_b) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
-    for (int h : dense_w) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
-    stats[1] += (nb ? 1 : 0) + (nw ? 1 : 0);
-    stats[12] += nb + nw;
+    for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x})
+      for (int h : *ids) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
+    stats[1] += (nb ? 1 : 0) + (nw ? 1 : 0) + (nx ? 1 : 0);
+    stats[12] += nb + nw + nx;
     stats[13] += t;
     stats[2] += (double)ss[SS_STEPS];
-    stats[4] += (double)ss[SS_FOUT] + (nb + nw);  // frontier in = previous frontier out (+ initial)
-    stats[5] += (double)ss[SS_CAND];
+    stats[4] += (double)ss[SS_FOUT] + (nb + nw + nx);  // frontier in = previous frontier out (+ initial)
     stats[6] += (double)ss[SS_FOUT];
-    if (debug())
-      fprintf(stderr, "[lincheck] dense: %d block-team + %d wave-team histories (grids %d/%d): %.3f ms, "
-              "steps=%llu cand=%llu Fout=%llu\n", nb, nw, std::min(dgrid_b, nb), std::min(dgrid_w, (nw + 15) / 16), t,
-              ss[SS_STEPS], ss[SS_CAND], ss[SS_FOUT]);
+    if (debug()) {
+      fprintf(stderr, "[lincheck] dense: %d block + %d wave + %d wide (%d teams x %d) histories: %.3f ms, "
+              "steps=%llu Fout=%llu\n", nb, nw, nx, teams, G, t, ss[SS_STEPS], ss[SS_FOUT]);
+      dense_report();
+    }
     return 0;
+  }
+
+  // LC_DEBUG: per-team spans and the slowest histories (s_memrealtime, 100 MHz)
+  void dense_report() {
+    const int n = enc.n_hist;
+    std::vector<unsigned long long> T((size_t)n * 2);
+    if (hipMemcpy(T.data(), d_dstamps.p, T.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    const std::vector<int>* lists[3] = {&dense_b, &dense_w, &dense_x};
+    const char* names[3] = {"block", "wave", "wide"};
+    unsigned long long t0 = ~0ull;
+    for (auto* ids : lists)
+      for (int h : *ids) t0 = std::min(t0, T[2 * h]);
+    for (int team = 0; team < 3; ++team) {
+      const std::vector<int>& ids = *lists[team];
+      if (ids.empty()) continue;
+      unsigned long long first = ~0ull, last = 0;
+      double by_l_us[64] = {0}, by_l_steps[64] = {0};
+      std::vector<std::pair<double, int>> dur;
+      for (int h : ids) {
+        first = std::min(first, T[2 * h]);
+        last = std::max(last, T[2 * h + 1]);
+        const double us = (double)(T[2 * h + 1] - T[2 * h]) / 100.0;
+        dur.push_back({us, h});
+        by_l_us[enc.live_max[h]] += us;
+        by_l_steps[enc.live_max[h]] += enc.n_steps(h);
+      }
+      std::sort(dur.rbegin(), dur.rend());
+      fprintf(stderr, "[lincheck]   %s teams: start %.1f us, end %.1f us after the first dequeue\n", names[team],
+              (first - t0) / 100.0, (last - t0) / 100.0);
+      for (int i = 0; i < (int)dur.size() && i < 4; ++i) {
+        const int h = dur[i].second;
+        fprintf(stderr, "[lincheck]     slowest #%d: h=%d width=%d steps=%d %.1f us (start %.1f)\n", i, h,
+                enc.live_max[h], enc.n_steps(h), dur[i].first, (T[2 * h] - t0) / 100.0);
+      }
+      for (int l = 0; l < 64; ++l)
+        if (by_l_steps[l] > 0)
+          fprintf(stderr, "[lincheck]     width %2d: %.3f us per step over %.0f steps\n", l,
+                  by_l_us[l] / by_l_steps[l], by_l_steps[l]);
+    }
   }
 
   int ensure_grid(int nh) {
@@ -694,13 +793,14 @@ struct lc_plan {
     int rc = 0;
     std::vector<int> grid_ids;
     const bool keys = max_t == INT32_MAX && path == 1;
-    const bool dense = max_t == INT32_MAX && path == 0 && (dense_b.size() + dense_w.size()) > 0;
+    const bool dense = max_t == INT32_MAX && path == 0 && (dense_b.size() + dense_w.size() + dense_x.size()) > 0;
     std::vector<char> done(enc.n_hist, 0);
     if (dense) {
       rc = run_dense(&ms);
       if (rc) return rc;
       for (int h : dense_b) done[h] = 1;
       for (int h : dense_w) done[h] = 1;
+      for (int h : dense_x) done[h] = 1;
     }
     if (keys) {
       rc = run_keys(&ms);

@@ -262,8 +262,8 @@ def _live_width(h, k):
 
 
 def test_gpu_dense_tables_vs_oracle():
-    """Dense closure tables (dense.hip): wave teams (width <= 12), workgroup teams (13..17)
-    and the wide histories routed to the grid kernel, in one batch, bit-exact with the oracle."""
+    """Dense closure tables (dense.hip): wave teams (width <= 11), workgroup teams (12..17)
+    and wide teams (18..22, HBM tables), in one batch, bit-exact with the oracle."""
     hs = [synth.gen_register_keys(28, 1000, 5, 0.01, config_id=3, invalid_keys=(2, 9, 20))]
     hs += [synth.gen_register(150, 5, 0.12, 31000 + t, invalid=(t % 2 == 0)) for t in range(6)]
     h = H.concat(hs)
@@ -273,11 +273,65 @@ def test_gpu_dense_tables_vs_oracle():
     p.run()
     g = p.results()
     s = p.stats()
-    assert s["dense_histories"] == sum(w <= 17 for w in widths)
+    assert s["dense_histories"] == sum(w <= 22 for w in widths)
     exp = oracle.check_many("cas-register", h, n_threads=8)
     for k in range(h.n_hist):
         _cmp(g, exp[k], k, f"dense w={widths[k]}")
     assert any(e["valid"] == 0 for e in exp)
+    p.close()
+
+
+_WIDE = {}
+
+
+def _wide_batch():
+    """Short histories with many crashed ops: live widths 18..22 (wide teams), with their
+    oracle results (computed once per module)."""
+    if _WIDE:
+        return _WIDE["h"], _WIDE["widths"], _WIDE["exp"]
+    hs, widths = [], []
+    for t in range(60):
+        h = synth.gen_register(130, 5, 0.15, 52000 + t, invalid=(t % 3 == 0))
+        w = _live_width(h, 0)
+        if 18 <= w <= 22:
+            hs.append(h)
+            widths.append(w)
+        if len(hs) == 6:
+            break
+    assert len(hs) >= 4, widths
+    h = H.concat(hs)
+    _WIDE.update(h=h, widths=widths, exp=oracle.check_many("cas-register", h, n_threads=8))
+    return h, widths, _WIDE["exp"]
+
+
+@pytest.mark.parametrize("team", ["8x8", "2x1", "1x2"])
+def test_gpu_dense_wide_teams(team, monkeypatch):
+    """Wide teams: steps of width <= 17 on the leader's LDS table, wider steps on the team's
+    HBM table with one team barrier per layer. Team size and count must not change answers
+    (2x1: one two-workgroup team takes every history in turn; 1x2: leader-only teams)."""
+    g, teams = team.split("x")
+    monkeypatch.setenv("LC_WIDE_G", g)
+    monkeypatch.setenv("LC_WIDE_TEAMS", teams)
+    h, widths, exp = _wide_batch()
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    got = p.results()
+    assert p.stats()["dense_histories"] == h.n_hist
+    for k in range(h.n_hist):
+        _cmp(got, exp[k], k, f"wide {team} w={widths[k]}")
+    p.close()
+
+
+def test_gpu_dense_width_limit_routes_to_grid(monkeypatch):
+    """LC_DENSE_MAXW=17 sends the wide histories to the sparse grid kernel: same answers."""
+    h, widths, exp = _wide_batch()
+    monkeypatch.setenv("LC_DENSE_MAXW", "17")
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    got = p.results()
+    assert p.stats()["dense_histories"] == 0
+    for k in range(h.n_hist):
+        _cmp(got, exp[k], k, f"grid w={widths[k]}")
     p.close()
 
 
