@@ -37,7 +37,6 @@ namespace lc {
 namespace {
 
 constexpr int BINOM_N = 24;
-constexpr uint32_t OP_NONE = 0, OP_MOVE = 1, OP_MOVEU = 2, OP_IDENT = 3;
 constexpr int CMD_STEP = 1, CMD_EXIT = 2;
 
 typedef __attribute__((address_space(1))) uint64_t gu64;
@@ -56,17 +55,20 @@ struct TeamCtl {
   unsigned ops[32];
 };
 
-// decoded op: kind[0:4) | src[4:8) | dst[8:12)
+// decoded op, laid out for transfer(): srcsh[0:7) = 8 * source state, or OPF_FOLD (a write
+// reads every state); dstsh[8:14) = 8 * destination state; OPF_IDENT (read nil: every state
+// stays); OPF_NONE (the op names a value the register never holds: it moves nothing)
+constexpr uint32_t OPF_FOLD = 64u, OPF_IDENT = 1u << 16, OPF_NONE = 1u << 17;
 __device__ __forceinline__ uint32_t decode_op(uint32_t am, uint32_t bm) {
-  if (am == 0) return OP_NONE;  // precondition names a value the register never holds
+  if (am == 0) return OPF_NONE;  // precondition names a value the register never holds
   if (bm) {
-    const uint32_t dst = (uint32_t)__builtin_ctz(bm) << 8;
-    if (am == 0xffu) return OP_MOVEU | dst;  // write: from any state
-    return OP_MOVE | ((uint32_t)__builtin_ctz(am) << 4) | dst;
+    const uint32_t dst = ((uint32_t)__builtin_ctz(bm) * 8u) << 8;
+    if (am == 0xffu) return OPF_FOLD | dst;  // write: from any state
+    return (uint32_t)__builtin_ctz(am) * 8u | dst;
   }
-  if (am == 0xffu) return OP_IDENT;  // read nil: every state stays
-  const uint32_t a = (uint32_t)__builtin_ctz(am);
-  return OP_MOVE | (a << 4) | (a << 8);
+  if (am == 0xffu) return OPF_IDENT;  // read nil: every state stays
+  const uint32_t a = (uint32_t)__builtin_ctz(am) * 8u;
+  return a | (a << 8);
 }
 
 // positions (of 8) whose mask lacks bit k (k < 3), one byte / replicated over 8 bytes
@@ -75,22 +77,20 @@ __device__ __forceinline__ uint64_t keep64(int k) {
   return k == 0 ? 0x5555555555555555ull : k == 1 ? 0x3333333333333333ull : 0x0f0f0f0f0f0f0f0full;
 }
 
-// op applied to word a (all 8 states), result bytes kept at positions `keep` (8-bit,
-// replicated as keep_all), then moved up by `up` positions
+// op (wave-uniform) applied to word a (all 8 states), result bytes kept at positions
+// `keep` (8-bit, replicated as keep_all), then moved up by `up` positions. The flag tests
+// are scalar branches on a uniform value; the common MOVE path is shift, mask, shift.
 __device__ __forceinline__ uint64_t transfer(uint32_t op, uint64_t a, uint32_t keep, uint64_t keep_all, int up) {
-  const uint32_t kind = op & 15u;
-  if (kind == OP_IDENT) return (a & keep_all) << up;
+  if (op & (OPF_IDENT | OPF_NONE)) return (op & OPF_NONE) ? 0ull : (a & keep_all) << up;
   uint32_t t;
-  if (kind == OP_MOVE) {
-    t = (uint32_t)(a >> (((op >> 4) & 15u) * 8u));
-  } else if (kind == OP_MOVEU) {
+  if (op & OPF_FOLD) {
     t = (uint32_t)a | (uint32_t)(a >> 32);
     t |= t >> 16;
     t |= t >> 8;
   } else {
-    return 0;
+    t = (uint32_t)(a >> (op & 63u));
   }
-  return (uint64_t)(t & keep) << (((op >> 8) & 15u) * 8u + (uint32_t)up);
+  return (uint64_t)(t & keep) << (((op >> 8) & 63u) + (uint32_t)up);
 }
 
 // table access: LDS tables plainly, HBM team tables write-through sc1 / L1-bypassing sc1
