@@ -21,14 +21,14 @@
 // whose predecessors (one bit fewer) are final earlier, so R is the closure set of the
 // sparse search and popcount(R) its explored count, bit-exact.
 //
-// Teams (one history each, dequeued heaviest first from a global counter):
-//   WAVE  one wave, LDS table, widths <= 11 (256-thread workgroups beside the wide teams)
-//   BLOCK one 1024-thread workgroup, LDS table, widths 12..17
-//   WIDE  team_size workgroups: the leader runs steps of width <= 17 on its LDS table;
-//         wider steps run on an HBM table the whole team shares, one team barrier per
-//         layer. Every HBM table byte is stored sc1 (write-through) and loaded sc1
-//         (L1-bypassing), drained before each barrier arrival (cdna_hip_programming.md
-//         Guideline 16, MI355X_MICROARCH.md "Valid forms" row 1), so no fences are needed.
+// Teams:
+//   WAVE  one wave, LDS table, widths <= 11 (256-thread workgroups beside the big kernel)
+//   BLOCK one 1024-thread workgroup, LDS table, widths 12..17 (dequeued heaviest first)
+//   TILE  2^t workgroups for one history of width 17 + t, each holding one 17-bit tile of
+//         the table in LDS; cross-tile pulls go through per-tile HBM mirrors written sc1
+//         (write-through) and read sc1 (L1-bypassing), published by a per-layer token that
+//         every storing wave drained before (cdna_hip_programming.md Guideline 16,
+//         MI355X_MICROARCH.md "Valid forms" row 1), so no fences are needed.
 #include "dense.hpp"
 #include "device_common.hpp"
 #include "search.hpp"
@@ -93,11 +93,7 @@ __device__ __forceinline__ uint64_t transfer(uint32_t op, uint64_t a, uint32_t k
   return (uint64_t)(t & keep) << (((op >> 8) & 63u) + (uint32_t)up);
 }
 
-// table access: LDS tables plainly, HBM team tables write-through sc1 / L1-bypassing sc1
-struct LdsTab {
-  static __device__ __forceinline__ uint64_t ld(const uint64_t* p) { return *p; }
-  static __device__ __forceinline__ void st(uint64_t* p, uint64_t v) { *p = v; }
-};
+// HBM tile mirrors: write-through sc1 stores, L1-bypassing sc1 loads
 struct HbmTab {
   static __device__ __forceinline__ uint64_t ld(const uint64_t* p) {
     return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -107,36 +103,29 @@ struct HbmTab {
   }
 };
 
-// One step's hi pulls and in-word closure for word w; returns popcount(R).
+
+// One step's pulls and in-word closure for word w (LDS table B): R starts from R0 (pulls
+// from other tiles, computed by the caller), adds the pulls from the finalized words one
+// local hi bit below and the in-word closure. Returns popcount(R); *out = X | R.
 // opv: lane k holds slot k's decoded op (read with readlane, wave-uniform).
-template <int HMAX, int BATCH, class M>
+template <int HMAX, int BATCH>
 __device__ __forceinline__ uint32_t close_word(uint64_t* B, uint32_t w, uint32_t live, int j, int H,
-                                              uint32_t opv) {
-  const uint64_t X = M::ld(B + w);
-  uint64_t R = 0;
+                                              uint32_t opv, uint64_t R0, uint64_t* out) {
+  const uint64_t X = B[w];
+  uint64_t R = R0;
   const bool j_lo = j < 3;
   const uint32_t jh = j_lo ? 0u : 1u << (j - 3);
   const bool has_j = (w & jh) != 0;
-  // ---- pulls from the finalized words one hi bit below, BATCH loads in flight
-#pragma unroll
-  for (int b0 = 0; b0 < HMAX; b0 += BATCH) {
-    if (b0 >= H) break;
-    uint64_t v[BATCH];
-#pragma unroll
-    for (int i = 0; i < BATCH; ++i) {
-      const int b = b0 + i;
-      v[i] = 0;
-      if (b < H) {
-        const uint32_t bit = 1u << b;
-        const bool act = has_j ? (bit == jh) : ((w & bit) != 0);
-        if (act) v[i] = M::ld(B + (w ^ bit));
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < BATCH; ++i) {
-      const int b = b0 + i;
-      if (b < H) R |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, b + 3), v[i], 0xffu, ~0ull, 0);
-    }
+  // ---- pulls from the finalized words one hi bit below. A rolled loop with the op read by
+  // a uniform-index readlane: unrolling it keeps a 64-bit uniform mask live per bit, which
+  // spills the SGPRs into VGPR lanes and costs more than the loads it would overlap.
+#pragma unroll 2
+  for (int b = 0; b < H; ++b) {
+    const uint32_t bit = 1u << b;
+    const bool act = has_j ? (bit == jh) : ((w & bit) != 0);
+    uint64_t v = 0;
+    if (act) v = B[w ^ bit];
+    R |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, b + 3), v, 0xffu, ~0ull, 0);
   }
   if (!has_j) {
     const uint32_t notj = j_lo ? keep8(j) : 0xffu;
@@ -156,16 +145,18 @@ __device__ __forceinline__ uint32_t close_word(uint64_t* B, uint32_t w, uint32_t
     if (j_lo)  // the returning op, linearized last
       R |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, j), X | R, notj, notj64, 1 << j);
   }
-  if (R) M::st(B + w, X | R);
+  if (R) B[w] = X | R;
+  *out = X | R;
   return (uint32_t)__popcll(R);
 }
 
-// The closure layers of one step, words split over participants gt = 0..gn-1; sync() ends
-// every layer (the last one too: the return that follows reads the last layer's words).
-template <int HMAX, int BATCH, class M, class Sync>
+// The closure layers of one step on an LDS table, words split over the team's threads
+// tt = 0..nt-1; sync() ends every layer (the last one too: the return that follows reads
+// the last layer's words).
+template <int HMAX, int BATCH, class Sync>
 __device__ __forceinline__ unsigned long long run_layers(uint64_t* B, const uint32_t* words, const uint32_t* wofs,
                                                         const uint32_t* binom, uint32_t live, int j,
-                                                        uint32_t opv, int gt, int gn, Sync&& sync) {
+                                                        uint32_t opv, int tt, int nt, Sync&& sync) {
   const int L = 32 - __clz((int)live);
   const int H = L > 3 ? L - 3 : 0;
   const uint32_t live_hi = live >> 3;
@@ -173,20 +164,20 @@ __device__ __forceinline__ unsigned long long run_layers(uint64_t* B, const uint
   for (int q = 0; q <= H; ++q) {
     // words of popcount q below 2^H: a prefix of layer q of the sorted list
     const uint32_t nq = binom[H * BINOM_N + q], o = wofs[q];
-    for (uint32_t r = (uint32_t)gt; r < nq; r += (uint32_t)gn) {
+    for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)nt) {
       const uint32_t w = words[o + r];
       if (w & ~live_hi) continue;
-      expl += close_word<HMAX, BATCH, M>(B, w, live, j, H, opv);
+      uint64_t nv;
+      expl += close_word<HMAX, BATCH>(B, w, live, j, H, opv, 0ull, &nv);
     }
     sync();
   }
   return expl;
 }
 
-// Return slot j: the post-return frontier moves down to the masks without j. Returns the
-// OR of this participant's new words (nonzero = some config survived).
-template <class M>
-__device__ __forceinline__ uint64_t return_slot(uint64_t* B, uint32_t live, int j, int gt, int gn,
+// Return slot j < 17 on an LDS table: the post-return frontier moves down to the masks
+// without j. Returns the OR of this thread's new words (nonzero = some config survived).
+__device__ __forceinline__ uint64_t return_slot(uint64_t* B, uint32_t live, int j, int tt, int nt,
                                                unsigned long long& fout) {
   const int L = 32 - __clz((int)live);
   const int nwt = 1 << (L > 3 ? L - 3 : 0);
@@ -194,21 +185,21 @@ __device__ __forceinline__ uint64_t return_slot(uint64_t* B, uint32_t live, int 
   if (j < 3) {
     const uint64_t with_j = ~keep64(j);
     const int sh = 1 << j;
-    for (int w = gt; w < nwt; w += gn) {
-      const uint64_t v = (M::ld(B + w) & with_j) >> sh;
-      M::st(B + w, v);
+    for (int w = tt; w < nwt; w += nt) {
+      const uint64_t v = (B[w] & with_j) >> sh;
+      B[w] = v;
       anyv |= v;
       fout += __popcll(v);
     }
   } else {
     const int jb = 1 << (j - 3);
     const int half = nwt >> 1;
-    for (int x = gt; x < half; x += gn) {
+    for (int x = tt; x < half; x += nt) {
       const int lo = x & (jb - 1);
       const int w = ((x ^ lo) << 1) | lo;
-      const uint64_t v = M::ld(B + (w | jb));
-      M::st(B + w, v);
-      M::st(B + (w | jb), 0);
+      const uint64_t v = B[w | jb];
+      B[w] = v;
+      B[w | jb] = 0;
       anyv |= v;
       fout += __popcll(v);
     }
@@ -281,47 +272,24 @@ __device__ __forceinline__ uint32_t read_step(const StreamWin& sw, int64_t pos, 
   return H0;
 }
 
-template <int TEAM, int WG, int TLOG, bool GLOBAL_WORDS>
-__global__ void __launch_bounds__(WG) dense_kernel(DenseParams p) {
-  constexpr int NTEAM = WG / TEAM;
+// Histories dequeued one at a time by a team of TEAM threads (a wave or a workgroup) that
+// keeps the whole table in LDS (B, 2^(TLOG-3) words).
+template <int TEAM, int TLOG>
+__device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, uint32_t* opt, int* sQ,
+                                             unsigned long long* sExpl, const uint32_t* words,
+                                             const uint32_t* wofs, const uint32_t* binom, int tt,
+                                             unsigned long long& st_fout, unsigned long long& st_steps) {
   constexpr int HMAX = TLOG - 3;
-  constexpr int TWORDS = 1 << HMAX;  // u64 words per team
-  constexpr int LBITS = GLOBAL_WORDS ? DENSE_WORD_BITS : HMAX;
-  __shared__ uint64_t sTab[NTEAM * TWORDS];
-  __shared__ uint32_t sWords[GLOBAL_WORDS ? 1 : (1 << HMAX)];  // words sorted by (popcount, value)
-  __shared__ uint32_t sWOff[LBITS + 2];
-  __shared__ uint32_t sBinom[BINOM_N * BINOM_N];
-  __shared__ uint32_t sOp[NTEAM][32];  // decoded op per slot
-  __shared__ int sQ[NTEAM];
-  __shared__ unsigned long long sExpl[NTEAM];
-
-  const int tid = threadIdx.x;
-  const int team = tid / TEAM, tt = tid % TEAM, lane = tid & 63;
-  uint64_t* const B = &sTab[team * TWORDS];
-  uint32_t* const opt = sOp[team];
-  const uint32_t* const words = GLOBAL_WORDS ? p.words : sWords;
-
-  init_tables(sBinom, sWOff, LBITS, WG);
-  if constexpr (!GLOBAL_WORDS) {
-    for (int v = tid; v < (1 << HMAX); v += WG) {  // colex rank within its popcount layer
-      uint32_t rank = 0;
-      int i = 0;
-      for (uint32_t x = (uint32_t)v; x; x &= x - 1, ++i) rank += sBinom[__builtin_ctz(x) * BINOM_N + i + 1];
-      sWords[sWOff[__popc(v)] + rank] = (uint32_t)v;
-    }
-    __syncthreads();
-  }
-
-  unsigned long long st_fout = 0, st_steps = 0;
+  const int lane = threadIdx.x & 63;
   for (;;) {
-    if (tt == 0) sQ[team] = atomicAdd(p.queue, 1);
+    if (tt == 0) *sQ = atomicAdd(p.queue, 1);
     team_sync<TEAM>();
-    const int qi = sQ[team];
-    if (tt == 0) sExpl[team] = 0;
+    const int qi = *sQ;
+    if (tt == 0) *sExpl = 0;
     team_sync<TEAM>();
     if (qi >= p.n) break;
     const int h = p.order[qi];
-    if (p.stamps && tt == 0) p.stamps[2 * h] = __builtin_amdgcn_s_memrealtime();
+    if (p.stamps && tt == 0) p.stamps[4 * h] = __builtin_amdgcn_s_memrealtime();
     const int lmax = p.lmax[h];
     const int NW = lmax > 3 ? 1 << (lmax - 3) : 1;
     const int ns = p.nsteps[h];
@@ -341,9 +309,8 @@ __global__ void __launch_bounds__(WG) dense_kernel(DenseParams p) {
       const uint32_t live = H0 & 0x3fffffu;
       const int j = (int)((H0 >> 22) & 31u);
       const uint32_t opv = opt[lane & 31];  // lane k: slot k's op, read with readlane
-      expl += run_layers<HMAX, 4, LdsTab>(B, words, sWOff, sBinom, live, j, opv, tt, TEAM,
-                                          [] { team_sync<TEAM>(); });
-      const uint64_t anyv = return_slot<LdsTab>(B, live, j, tt, TEAM, st_fout);
+      expl += run_layers<HMAX, 4>(B, words, wofs, binom, live, j, opv, tt, TEAM, [] { team_sync<TEAM>(); });
+      const uint64_t anyv = return_slot(B, live, j, tt, TEAM, st_fout);
       ++st_steps;
       if (!team_any<TEAM>(anyv != 0)) {
         fail_t = t;
@@ -353,9 +320,9 @@ __global__ void __launch_bounds__(WG) dense_kernel(DenseParams p) {
     // explored: team reduction
     for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
     if constexpr (TEAM >= 256) {
-      if (lane == 0 && expl) atomicAdd(&sExpl[team], expl);
+      if (lane == 0 && expl) atomicAdd(sExpl, expl);
       __syncthreads();
-      expl = sExpl[team];
+      expl = *sExpl;
     } else {
       expl = __shfl(expl, 0, 64);
     }
@@ -363,17 +330,49 @@ __global__ void __launch_bounds__(WG) dense_kernel(DenseParams p) {
       p.explored[h] = expl;
       p.fail_step[h] = fail_t;
       p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
-      if (p.stamps) p.stamps[2 * h + 1] = __builtin_amdgcn_s_memrealtime();
+      if (p.stamps) p.stamps[4 * h + 1] = __builtin_amdgcn_s_memrealtime();
     }
     team_sync<TEAM>();
   }
-  // launch statistics (per wave, one atomic each)
-  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
-  if (lane == 0 && st_fout) atomicAdd(&p.stats[SS_FOUT], st_fout);
-  if (tt == 0 && st_steps) atomicAdd(&p.stats[SS_STEPS], st_steps);
 }
 
-// Team barrier over the team's G workgroups: every wave drains its (sc1) stores, one lane
+// launch statistics (per wave, one atomic each)
+__device__ __forceinline__ void flush_stats(const DenseParams& p, unsigned long long st_fout,
+                                            unsigned long long st_steps, bool step_owner) {
+  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
+  if ((threadIdx.x & 63) == 0 && st_fout) atomicAdd(&p.stats[SS_FOUT], st_fout);
+  if (step_owner && st_steps) atomicAdd(&p.stats[SS_STEPS], st_steps);
+}
+
+constexpr int WAVE_WG = 256;
+
+// WAVE teams: one history per wave, 4 waves per workgroup, tables of 2^DENSE_WAVE_LMAX masks.
+__global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
+  constexpr int NTEAM = WAVE_WG / 64;
+  constexpr int HMAX = DENSE_WAVE_LMAX - 3;
+  __shared__ uint64_t sTab[NTEAM << HMAX];
+  __shared__ uint32_t sWords[1 << HMAX];  // words sorted by (popcount, value)
+  __shared__ uint32_t sWOff[HMAX + 2];
+  __shared__ uint32_t sBinom[BINOM_N * BINOM_N];
+  __shared__ uint32_t sOp[NTEAM][32];
+  __shared__ int sQ[NTEAM];
+  __shared__ unsigned long long sExpl[NTEAM];
+  const int tid = threadIdx.x, team = tid / 64, tt = tid % 64;
+  init_tables(sBinom, sWOff, HMAX, WAVE_WG);
+  for (int v = tid; v < (1 << HMAX); v += WAVE_WG) {  // colex rank within its popcount layer
+    uint32_t rank = 0;
+    int i = 0;
+    for (uint32_t x = (uint32_t)v; x; x &= x - 1, ++i) rank += sBinom[__builtin_ctz(x) * BINOM_N + i + 1];
+    sWords[sWOff[__popc(v)] + rank] = (uint32_t)v;
+  }
+  __syncthreads();
+  unsigned long long st_fout = 0, st_steps = 0;
+  history_loop<64, DENSE_WAVE_LMAX>(p, &sTab[team << HMAX], sOp[team], &sQ[team], &sExpl[team], sWords, sWOff,
+                                    sBinom, tt, st_fout, st_steps);
+  flush_stats(p, st_fout, st_steps, tt == 0);
+}
+
+// Team barrier over a tile team's G workgroups: every wave drains its (sc1) stores, one lane
 // per workgroup adds to the arrival counter, the last arriver bumps the generation the
 // others poll (relaxed sc1 loads + s_sleep). A 20 s watchdog raises p.abort instead of
 // hanging. Returns false once aborted.
@@ -407,6 +406,36 @@ __device__ __forceinline__ bool team_bar(TeamCtl* c, int G, int32_t* abort_flag,
   return *s_abort == 0;
 }
 
+// thread 0 waits until every flag of `mask` (bit b -> flags[rank ^ (1 << b)]) reaches
+// token, then the workgroup proceeds (sc1 polls, s_sleep, 20 s watchdog).
+__device__ __forceinline__ void wait_flags(const DenseParams& p, unsigned long long* flags, int rank,
+                                           uint32_t mask, unsigned long long token, int* s_abort) {
+  if (threadIdx.x == 0 && mask) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    long spins = 0;
+    for (uint32_t m = mask; m;) {
+      const int b = __builtin_ctz(m);
+      if (ld_agent(&flags[rank ^ (1 << b)]) >= token) {
+        m &= m - 1;
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+          st_agent(p.abort, 1);
+          *s_abort = 1;
+          break;
+        }
+        if (ld_agent(p.abort)) {
+          *s_abort = 1;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, unsigned long long* s) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
   if (threadIdx.x == 0) *s = 0;
@@ -418,150 +447,233 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
   return r;
 }
 
-__global__ void __launch_bounds__(1024) dense_wide_kernel(DenseParams p) {
+// BLOCK histories and TILE teams in one launch (same 1024-thread, 128 KiB-LDS workgroups, so
+// every workgroup is resident: the grid never exceeds one workgroup per CU).
+//
+// A TILE team checks one history of width 17 + t with G = 2^t workgroups. Workgroup r holds
+// tile r: the masks whose slots 17..17+t-1 spell r, over the low 17 slots, in its LDS. The
+// leader (r = 0) runs every step of width <= 17 alone (the other tiles are empty then);
+// wider steps run on every tile. Tile r's word w pulls from its own words (local bits) and
+// from word w of tiles r \ b (bits b of r), which are final once tile r \ b finished the
+// same local layer: each tile publishes every finished word to its HBM mirror (sc1 stores,
+// in word-list order, so a wave's stores and a successor's loads are contiguous) and then
+// its layer token (flags[r] = step << 5 | layer + 1), and successors poll the
+// tokens of their predecessors — point-to-point, one hop per team bit, instead of a team
+// barrier per layer. Returning a team slot j: tiles without j take tile r | j's mirror.
+__global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   constexpr int HSOLO = DENSE_LMAX - 3;
-  constexpr int HTEAM = DENSE_WORD_BITS;
   __shared__ uint64_t sTab[1 << HSOLO];
   __shared__ uint32_t sWOff[DENSE_WORD_BITS + 2];
   __shared__ uint32_t sBinom[BINOM_N * BINOM_N];
   __shared__ uint32_t sOp[32];
-  __shared__ int sQ, sCmd, sH, sAbort;
+  __shared__ int sQ, sCmd, sAbort;
   __shared__ long long sPos;
   __shared__ unsigned sAny;
   __shared__ unsigned long long sRed;
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int G = p.team_size;
-  const int team = blockIdx.x / G, rank = blockIdx.x % G;
-  TeamCtl* const ctl = (TeamCtl*)p.ctl + team;
-  uint64_t* const GT = p.gtab + ((size_t)team << DENSE_WORD_BITS);
-  const int gt = rank * 1024 + tid, gn = G * 1024;
   init_tables(sBinom, sWOff, DENSE_WORD_BITS, 1024);
   if (tid == 0) sAbort = 0;
   __syncthreads();
-  unsigned long long expl = 0, st_fout = 0, st_steps = 0;
-  auto bar = [&]() { return team_bar(ctl, G, p.abort, &sAbort); };
+  unsigned long long st_fout = 0, st_steps = 0;
 
-  // one team step on the HBM table (every rank; the ops are in sOp); returns "survived"
-  auto team_step = [&](long long pos) -> bool {
-    const uint32_t H0 = p.stream[pos];
+  if ((int)blockIdx.x >= p.n_team_wgs) {  // ------------------------------- BLOCK histories
+    history_loop<1024, DENSE_LMAX>(p, sTab, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout, st_steps);
+    flush_stats(p, st_fout, st_steps, tid == 0);
+    return;
+  }
+
+  // ------------------------------------------------------------------------- TILE team
+  const int team = p.wg_team[blockIdx.x];
+  const int base = p.team_base[team];
+  const int rank = (int)blockIdx.x - base;
+  const int G = 1 << p.team_bits[team];
+  const int h = p.team_hist[team];
+  TeamCtl* const ctl = (TeamCtl*)p.ctl + team;
+  unsigned long long* const flags = p.flags + base;
+  auto mirror = [&](int r) { return p.mirror + ((size_t)(base + r) << HSOLO); };
+  uint64_t* const mine = mirror(rank);
+  auto bar = [&]() { return team_bar(ctl, G, p.abort, &sAbort); };
+  unsigned long long expl = 0, stepctr = 0;
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};  // LC_DEBUG phase cycles (wait, compute, publish, return, barrier, steps)
+  auto now = []() { return __builtin_amdgcn_s_memrealtime(); };
+
+  for (int i = tid; i < (1 << HSOLO); i += 1024) sTab[i] = 0;
+  __syncthreads();
+  if (rank == 0 && tid == 0) sTab[0] = 1;  // (cas-register) starts at nil: state id 0
+
+  // one step of width > 17 on every tile (the ops are in sOp); returns "survived"
+  auto team_step = [&](long long hpos) -> bool {
+    ++stepctr;
+    const unsigned long long tok0 = stepctr << 5;
+    const uint32_t H0 = p.stream[hpos];
     const uint32_t live = H0 & 0x3fffffu;
     const int j = (int)((H0 >> 22) & 31u);
     const uint32_t opv = sOp[lane & 31];
-    expl += run_layers<HTEAM, 8, HbmTab>(GT, p.words, sWOff, sBinom, live, j, opv, gt, gn, [&] { bar(); });
-    const uint64_t a = return_slot<HbmTab>(GT, live, j, gt, gn, st_fout);
-    if (__syncthreads_or(a != 0) && tid == 0)
+    const uint32_t live_loc = live & ((1u << DENSE_LMAX) - 1), live_team = live >> DENSE_LMAX;
+    const bool active = ((uint32_t)rank & ~live_team) == 0;
+    const int jt = j >= DENSE_LMAX ? j - DENSE_LMAX : -1;
+    const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
+    const int Lloc = live_loc ? 32 - __clz((int)live_loc) : 0;
+    const int H = Lloc > 3 ? Lloc - 3 : 0;
+    const uint32_t live_hi = live_loc >> 3;
+    // tiles this one pulls from: r \ b for its team bits (only r \ j when r holds j)
+    const uint32_t preds = tile_j ? (1u << jt) : ((uint32_t)rank & live_team);
+    const bool jloc_hi = j >= 3 && j < DENSE_LMAX;
+    uint64_t anyv = 0;
+    ph[5] += 1;
+    if (active) {
+      // mirror position of layer q's first word: words below 2^H in (popcount, value) order,
+      // so positions stay below 2^H <= 2^(DENSE_LMAX-3), the mirror's size
+      uint32_t mo = 0;
+      for (int q = 0; q <= H; ++q) {
+        unsigned long long tp = now();
+        wait_flags(p, flags, rank, preds, tok0 + q + 1, &sAbort);
+        ph[0] += now() - tp;
+        tp = now();
+        const uint32_t nq = sBinom[H * BINOM_N + q], o = sWOff[q];
+        for (uint32_t r = (uint32_t)tid; r < nq; r += 1024) {
+          const uint32_t w = p.words[o + r];
+          if (w & ~live_hi) continue;
+          // pulls from the tiles one team bit below: none for masks holding a local j
+          // (configs holding j are never expanded); a tile holding j takes only T_j of r \ j
+          uint64_t R0 = 0;
+          if (tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u))) {
+            for (uint32_t m = preds; m; m &= m - 1) {
+              const int b = __builtin_ctz(m);
+              const uint64_t v = HbmTab::ld(mirror(rank ^ (1 << b)) + mo + r);
+              R0 |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, DENSE_LMAX + b), v, 0xffu, ~0ull, 0);
+            }
+          }
+          uint64_t nv;
+          if (tile_j) {  // every mask here holds j: linearized last, from tile r \ j
+            const uint64_t X = sTab[w];
+            nv = X | R0;
+            if (R0) sTab[w] = nv;
+            expl += (uint32_t)__popcll(R0);
+          } else {
+            expl += close_word<HSOLO, 4>(sTab, w, live_loc, j, H, opv, R0, &nv);
+          }
+          if (!(p.dbg & 1)) HbmTab::st(mine + mo + r, nv);  // mirrors are in word-list order
+        }
+        mo += nq;
+        __syncthreads();
+        ph[1] += now() - tp;
+        tp = now();
+        // layer q published: every wave drains its sc1 stores, then one lane signals
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) st_agent(&flags[rank], tok0 + q + 1);
+        ph[2] += now() - tp;
+      }
+      const unsigned long long tr = now();
+      // return j
+      if (jt < 0) {
+        anyv = return_slot(sTab, live_loc, j, tid, 1024, st_fout);
+      } else if (tile_j) {  // this tile's masks all hold j: they move to tile r \ j
+        for (int w = tid; w < (1 << H); w += 1024) sTab[w] = 0;
+      } else {  // take tile r | j (final once its last layer is published)
+        wait_flags(p, flags, rank, 1u << jt, tok0 + H + 1, &sAbort);
+        const uint64_t* src = mirror(rank | (1 << jt));
+        // the words below 2^H are the first C(H, q) entries of every layer of the list
+        uint32_t mo = 0;
+        for (int q = 0; q <= H; ++q) {
+          const uint32_t nq = sBinom[H * BINOM_N + q], o = sWOff[q];
+          for (uint32_t r = (uint32_t)tid; r < nq; r += 1024) {
+            const uint32_t w = p.words[o + r];
+            const uint64_t v = (w & ~live_hi) ? 0ull : HbmTab::ld(src + mo + r);
+            sTab[w] = v;
+            anyv |= v;
+            st_fout += __popcll(v);
+          }
+          mo += nq;
+        }
+      }
+      ph[3] += now() - tr;
+    }
+    const unsigned long long tb = now();
+    if (__syncthreads_or(anyv != 0) && tid == 0)
       __hip_atomic_fetch_or(&ctl->any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bar();
+    bar();  // every tile done with this step (mirrors may be rewritten after this)
     if (tid == 0) sAny = ld_agent(&ctl->any);
     __syncthreads();
+    ph[4] += now() - tb;
     return sAny != 0;
   };
 
   if (rank == 0) {  // ---------------------------------------------------------- leader
-    for (;;) {
-      if (tid == 0) sQ = atomicAdd(p.queue, 1);
+    if (p.stamps && tid == 0) p.stamps[4 * h] = __builtin_amdgcn_s_memrealtime();
+    const int ns = p.nsteps[h];
+    unsigned long long team_cycles = 0, team_steps = 0;
+    StreamWin sw;
+    long long pos = p.sbeg[h];
+    int fail_t = -1;
+    for (int t = 0; t < ns && !sAbort; ++t) {
+      sw.need(p, pos, lane);
+      int ninv;
+      const uint32_t H0 = read_step(sw, pos, lane, tid < 64, sOp, &ninv);
+      const long long hpos = pos;
+      pos += 1 + ninv;
       __syncthreads();
-      const int qi = sQ;
-      __syncthreads();
-      if (qi >= p.n || sAbort) {
-        if (tid == 0) st_agent(&ctl->cmd, CMD_EXIT);
-        bar();
+      const uint32_t live = H0 & 0x3fffffu;
+      const int j = (int)((H0 >> 22) & 31u);
+      bool survived;
+      if ((live >> DENSE_LMAX) == 0) {  // narrow step: the leader alone (other tiles empty)
+        const uint32_t opv = sOp[lane & 31];
+        expl += run_layers<HSOLO, 4>(sTab, p.words, sWOff, sBinom, live, j, opv, tid, 1024,
+                                     [] { __syncthreads(); });
+        survived = __syncthreads_or(return_slot(sTab, live, j, tid, 1024, st_fout) != 0);
+      } else {  // wide step: every tile
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0) {
+          st_agent(&ctl->cmd, CMD_STEP);
+          st_agent(&ctl->pos, hpos);
+          st_agent(&ctl->any, 0u);
+        }
+        if (tid < 32) st_agent(&ctl->ops[tid], sOp[tid]);
+        if (!bar()) break;
+        survived = team_step(hpos);
+        team_cycles += __builtin_amdgcn_s_memrealtime() - t0;
+        ++team_steps;
+      }
+      if (tid == 0) ++st_steps;
+      if (!survived) {
+        fail_t = t;
         break;
       }
-      const int h = p.order[qi];
-      if (p.stamps && tid == 0) p.stamps[2 * h] = __builtin_amdgcn_s_memrealtime();
-      const int ns = p.nsteps[h];
-      for (int i = tid; i < (1 << HSOLO); i += 1024) sTab[i] = 0;
-      for (int i = tid; i < (1 << (p.lmax[h] - 3)); i += 1024) HbmTab::st(GT + i, 0);
-      __syncthreads();
-      if (tid == 0) sTab[0] = 1;  // (cas-register) starts at nil: state id 0
-      bool team_mode = false;
-      StreamWin sw;
-      long long pos = p.sbeg[h];
-      int fail_t = -1;
-      for (int t = 0; t < ns; ++t) {
-        sw.need(p, pos, lane);
-        int ninv;
-        const uint32_t H0 = read_step(sw, pos, lane, tid < 64, sOp, &ninv);
-        const long long hpos = pos;
-        pos += 1 + ninv;
-        __syncthreads();
-        const uint32_t live = H0 & 0x3fffffu;
-        const int j = (int)((H0 >> 22) & 31u);
-        const int L = 32 - __clz((int)live);
-        bool survived;
-        if (L <= DENSE_LMAX) {  // narrow step: the leader alone, LDS table
-          if (team_mode) {
-            for (int i = tid; i < (1 << HSOLO); i += 1024) sTab[i] = HbmTab::ld(GT + i);
-            __syncthreads();
-            team_mode = false;
-          }
-          const uint32_t opv = sOp[lane & 31];
-          expl += run_layers<HSOLO, 4, LdsTab>(sTab, p.words, sWOff, sBinom, live, j, opv, tid, 1024,
-                                               [] { __syncthreads(); });
-          survived = __syncthreads_or(return_slot<LdsTab>(sTab, live, j, tid, 1024, st_fout) != 0);
-        } else {  // wide step: the whole team, HBM table
-          if (!team_mode) {  // masks >= 2^17 are all empty: only the LDS part moves
-            for (int i = tid; i < (1 << HSOLO); i += 1024) HbmTab::st(GT + i, sTab[i]);
-            team_mode = true;
-          }
-          if (tid == 0) {
-            st_agent(&ctl->cmd, CMD_STEP);
-            st_agent(&ctl->h, h);
-            st_agent(&ctl->pos, hpos);
-            st_agent(&ctl->any, 0u);
-          }
-          if (tid < 32) st_agent(&ctl->ops[tid], sOp[tid]);
-          if (!bar()) break;
-          survived = team_step(hpos);
-        }
-        if (tid == 0) ++st_steps;
-        if (!survived) {
-          fail_t = t;
-          break;
-        }
-      }
-      const unsigned long long e = block_sum(expl, &sRed);
-      expl = 0;
-      if (tid == 0) {
-        if (e) atomicAdd(&p.explored[h], e);
-        p.fail_step[h] = fail_t;
-        p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
-        if (p.stamps) p.stamps[2 * h + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (tid == 0) st_agent(&ctl->cmd, CMD_EXIT);
+    bar();
+    const unsigned long long e = block_sum(expl, &sRed);
+    if (tid == 0) {
+      if (e) atomicAdd(&p.explored[h], e);
+      p.fail_step[h] = fail_t;
+      p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      if (p.stamps) {
+        p.stamps[4 * h + 1] = __builtin_amdgcn_s_memrealtime();
+        p.stamps[4 * h + 2] = team_cycles;
+        p.stamps[4 * h + 3] = team_steps;
       }
     }
   } else {  // ----------------------------------------------------------------- worker
-    int cur_h = -1;
     for (;;) {
       const bool ok = bar();
       if (tid == 0) {
         sCmd = ok ? ld_agent(&ctl->cmd) : CMD_EXIT;
-        sH = ld_agent(&ctl->h);
         sPos = ld_agent(&ctl->pos);
       }
       if (tid < 32) sOp[tid] = ld_agent(&ctl->ops[tid]);
       __syncthreads();
-      const int cmd = sCmd, h = sH;
-      const long long pos = sPos;
-      if (cmd != CMD_STEP || h != cur_h) {  // this rank's share of the previous history
-        const unsigned long long e = block_sum(expl, &sRed);
-        expl = 0;
-        if (tid == 0 && e && cur_h >= 0) atomicAdd(&p.explored[cur_h], e);
-        cur_h = h;
-      }
-      if (cmd != CMD_STEP) break;
-      team_step(pos);
+      if (sCmd != CMD_STEP) break;
+      team_step(sPos);
     }
+    const unsigned long long e = block_sum(expl, &sRed);
+    if (tid == 0 && e) atomicAdd(&p.explored[h], e);
   }
-  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
-  if (lane == 0 && st_fout) atomicAdd(&p.stats[SS_FOUT], st_fout);
-  if (tid == 0 && st_steps) atomicAdd(&p.stats[SS_STEPS], st_steps);
+  if (p.tstamps && tid == 0)
+    for (int i = 0; i < 6; ++i) p.tstamps[blockIdx.x * 8 + i] = ph[i];
+  flush_stats(p, st_fout, st_steps, tid == 0);
 }
-
-constexpr int WAVE_WG = 256;
-#define WAVE_KERNEL dense_kernel<64, WAVE_WG, DENSE_WAVE_LMAX, false>
-#define BLOCK_KERNEL dense_kernel<1024, 1024, DENSE_LMAX, true>
 
 }  // namespace
 
@@ -581,22 +693,19 @@ int dense_grid_size(DenseTeam kind) {
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
   int per_cu = 0;
   hipError_t e = kind == DENSE_WAVE
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, WAVE_KERNEL, WAVE_WG, 0)
-      : kind == DENSE_BLOCK ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, BLOCK_KERNEL, 1024, 0)
-                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_wide_kernel, 1024, 0);
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_wave_kernel, WAVE_WG, 0)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_big_kernel, 1024, 0);
   if (e != hipSuccess || per_cu < 1) return 0;
-  // wave teams: one workgroup per CU beside a wide team (the wide team's LDS leaves room);
-  // wide teams: one workgroup per CU, every workgroup of a team resident at once
-  return prop.multiProcessorCount * (kind == DENSE_BLOCK ? per_cu : 1);
+  // wave teams: one workgroup per CU beside a big-kernel workgroup (whose LDS leaves room);
+  // big kernel: one workgroup per CU, so every tile team is resident at once
+  return prop.multiProcessorCount;
 }
 
 hipError_t launch_dense(const DenseParams& p, DenseTeam kind, int grid, hipStream_t stream) {
   if (kind == DENSE_WAVE)
-    hipLaunchKernelGGL(WAVE_KERNEL, dim3(grid), dim3(WAVE_WG), 0, stream, p);
-  else if (kind == DENSE_BLOCK)
-    hipLaunchKernelGGL(BLOCK_KERNEL, dim3(grid), dim3(1024), 0, stream, p);
+    hipLaunchKernelGGL(dense_wave_kernel, dim3(grid), dim3(WAVE_WG), 0, stream, p);
   else
-    hipLaunchKernelGGL(dense_wide_kernel, dim3(grid), dim3(1024), 0, stream, p);
+    hipLaunchKernelGGL(dense_big_kernel, dim3(grid), dim3(1024), 0, stream, p);
   return hipGetLastError();
 }
 

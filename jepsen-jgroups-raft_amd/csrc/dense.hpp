@@ -16,7 +16,7 @@ namespace lc {
 
 constexpr int DENSE_LMAX = 17;       // widest table a workgroup holds in LDS (128 KiB)
 constexpr int DENSE_WAVE_LMAX = 11;  // histories this narrow run one per wave
-constexpr int DENSE_WIDE_LMAX = 22;  // widest table a team of workgroups keeps in HBM (4 MiB)
+constexpr int DENSE_WIDE_LMAX = 22;  // widest table a tile team holds (2^(22-17) LDS tiles)
 constexpr int DENSE_MAX_STATES = 8;  // register values (state ids) per history
 constexpr int DENSE_WORD_BITS = DENSE_WIDE_LMAX - 3;  // bits of the sorted word list
 
@@ -39,19 +39,28 @@ struct DenseParams {
   int32_t* fail_step;           // [n_hist]
   unsigned long long* explored; // [n_hist] (wide teams add into it: zeroed before launch)
   unsigned long long* stats;    // [SS_N] frontier-out, steps
-  unsigned long long* stamps;   // [n_hist][2] start / end (s_memrealtime, 100 MHz); may be null
-  // wide teams only
-  int32_t team_size;            // workgroups per team
-  uint64_t* gtab;               // [teams][2^DENSE_WORD_BITS] HBM tables
+  unsigned long long* stamps;   // [n_hist][4] start, end, team-step time (s_memrealtime, 100 MHz),
+                                // team steps; may be null
+  // tile teams (big kernel): workgroups [0, n_team_wgs) form the teams, the rest run the
+  // BLOCK histories of order[0..n)
+  int32_t n_team_wgs;
+  const int32_t* wg_team;       // [n_team_wgs] team of each workgroup
+  const int32_t* team_base;     // [teams] first workgroup
+  const int8_t* team_bits;      // [teams] t: 2^t workgroups, history width <= 17 + t
+  const int32_t* team_hist;     // [teams] history id
+  uint64_t* mirror;             // [n_team_wgs][2^(DENSE_LMAX-3)] published tile words
+  unsigned long long* flags;    // [n_team_wgs] layer tokens (zeroed before launch)
   void* ctl;                    // [teams] TeamCtl (zeroed before launch)
-  int32_t* abort;               // set when a team barrier times out
+  int32_t* abort;               // set when a team barrier / token wait times out
+  unsigned long long* tstamps;  // [n_team_wgs][8] LC_DEBUG phase cycles of each tile workgroup
+  int32_t dbg;                  // LC_DENSE_DBG experiment bits (timing only; 0 in production)
 };
 
-// Team kinds: WAVE = 256-thread workgroups, one history per wave (width <= DENSE_WAVE_LMAX);
-// BLOCK = 1024-thread workgroup per history, LDS table (width <= DENSE_LMAX);
-// WIDE = team_size 1024-thread workgroups per history: steps of width <= DENSE_LMAX run on
-// the leader's LDS table, wider steps on an HBM table shared by the team.
-enum DenseTeam { DENSE_WAVE = 0, DENSE_BLOCK = 1, DENSE_WIDE = 2 };
+// Kernels: WAVE = 256-thread workgroups, one history per wave (width <= DENSE_WAVE_LMAX);
+// BIG = 1024-thread workgroups: tile teams (one history of width 18..DENSE_WIDE_LMAX each,
+// one workgroup per 17-bit LDS tile) and BLOCK histories (width <= DENSE_LMAX, one
+// workgroup each, LDS table) in the same launch.
+enum DenseTeam { DENSE_WAVE = 0, DENSE_BIG = 1 };
 hipError_t launch_dense(const DenseParams& p, DenseTeam kind, int grid, hipStream_t stream);
 int dense_grid_size(DenseTeam kind);
 size_t dense_ctl_bytes();  // per team

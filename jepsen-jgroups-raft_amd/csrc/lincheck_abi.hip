@@ -128,12 +128,12 @@ struct lc_plan {
   // dense closure tables (narrow cas-register histories; dense.hpp)
   std::vector<int> dense_b, dense_w, dense_x;  // block / wave / wide teams, heaviest first
   DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dwords, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
-  DevArray d_dstamps, d_gtab, d_ctl, d_abort;
+  DevArray d_dstamps, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_thist;
   int64_t dstream_words = 0;
-  int dgrid_b = 0, dgrid_w = 0, dgrid_x = 0;
-  int wide_g = 8, wide_teams = 8, dense_maxw = DENSE_WIDE_LMAX;  // LC_WIDE_G / LC_WIDE_TEAMS / LC_DENSE_MAXW
-  hipStream_t stream2 = nullptr, stream3 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+  int dgrid_b = 0, dgrid_w = 0;
+  int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool spill_clean = false, kspill_clean = false;
   // results
   std::vector<int32_t> status, fail_step;
@@ -150,9 +150,7 @@ struct lc_plan {
     if (ev1) hipEventDestroy(ev1);
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_join) hipEventDestroy(ev_join);
-    if (ev_join2) hipEventDestroy(ev_join2);
     if (stream2) hipStreamDestroy(stream2);
-    if (stream3) hipStreamDestroy(stream3);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -204,12 +202,9 @@ struct lc_plan {
     if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
     if (!ev_fork) HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     if (!ev_join) HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-    if (!stream3) HIP_TRY(hipStreamCreateWithFlags(&stream3, hipStreamNonBlocking));
-    if (!ev_join2) HIP_TRY(hipEventCreateWithFlags(&ev_join2, hipEventDisableTiming));
     nwg = search_grid_size(model);
-    dgrid_b = dense_grid_size(DENSE_BLOCK);
+    dgrid_b = dense_grid_size(DENSE_BIG);
     dgrid_w = dense_grid_size(DENSE_WAVE);
-    dgrid_x = dense_grid_size(DENSE_WIDE);
     knwg = keys_grid_size(model);
     if (nwg <= 0 || knwg <= 0) {
       last_error = "search kernels cannot be resident (occupancy 0)";
@@ -219,9 +214,8 @@ struct lc_plan {
     if (e && !strcmp(e, "keys")) path = 1;
     if (e && !strcmp(e, "grid")) path = 2;
     if (e && !strcmp(e, "dense")) path = 0;
-    // dense-path knobs (tests): wide-team size and count, widest history the tables take
-    if ((e = getenv("LC_WIDE_G")) && atoi(e) > 0) wide_g = atoi(e);
-    if ((e = getenv("LC_WIDE_TEAMS")) && atoi(e) > 0) wide_teams = atoi(e);
+    // dense-path knobs (tests): workgroups tile teams may take per launch, widest history
+    if ((e = getenv("LC_TILE_WGS")) && atoi(e) > 0) tile_cap = atoi(e);
     if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
     // test hooks: shrink the keys kernel's per-workgroup capacities to force the fallback
     if ((e = getenv("LC_KCAP")) && atoll(e) > 0) kfcap = klcap = atoll(e);
@@ -273,7 +267,7 @@ struct lc_plan {
     dense_b.clear();
     dense_w.clear();
     dense_x.clear();
-    if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0 || dgrid_x <= 0) return 0;
+    if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0) return 0;
     const int n = enc.n_hist;
     std::vector<uint32_t> words;
     std::vector<int64_t> sbeg(n, 0);
@@ -331,9 +325,9 @@ struct lc_plan {
     return 0;
   }
 
-  // Dense closure-table kernels on three streams: wide teams first (every workgroup of a
-  // team must be resident), block teams beside them, wave teams filling the room the
-  // block teams leave on each CU.
+  // Dense closure-table kernels: the big kernel (tile teams first, then BLOCK histories) on
+  // one stream, the wave kernel beside it on a second stream. Wide histories whose tile
+  // teams do not fit one launch (tile_cap workgroups) run in further big-kernel launches.
   int run_dense(float* ms) {
     const int nb = (int)dense_b.size(), nw = (int)dense_w.size(), nx = (int)dense_x.size();
     if (nb + nw + nx == 0) return 0;
@@ -354,37 +348,56 @@ struct lc_plan {
     p.explored = d_dexpl.as<unsigned long long>();
     p.stats = d_stats.as<unsigned long long>();
     p.stamps = nullptr;
+    if (const char* e = getenv("LC_DENSE_DBG")) p.dbg = atoi(e);
     if (debug()) {
-      HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 16));
-      HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 16, stream));
+      HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
+      HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
       p.stamps = d_dstamps.as<unsigned long long>();
     }
-    const int G = std::max(1, std::min(wide_g, dgrid_x));
-    int teams = 0;
-    if (nx) {
-      teams = std::max(1, std::min(std::min(nx, wide_teams), dgrid_x / G));
-      HIP_TRY(d_gtab.ensure(((size_t)teams << DENSE_WORD_BITS) * 8));
-      HIP_TRY(d_ctl.ensure((size_t)teams * dense_ctl_bytes()));
+    // tile teams: one per wide history, 2^(width - 17) workgroups; packed into launches of at
+    // most `cap` workgroups (the first launch also runs the BLOCK histories)
+    const int cap = std::max(1, std::min(tile_cap, dgrid_b));
+    std::vector<std::vector<int>> launches(1);
+    int used = 0;
+    for (int h : dense_x) {
+      const int g = 1 << (enc.live_max[h] - DENSE_LMAX);
+      if (used + g > cap && !launches.back().empty()) {
+        launches.emplace_back();
+        used = 0;
+      }
+      launches.back().push_back(h);
+      used += g;
+    }
+    size_t max_wgs = 0, max_teams = 0;
+    std::vector<std::vector<int32_t>> l_wgteam(launches.size()), l_base(launches.size()), l_hist(launches.size());
+    std::vector<std::vector<int8_t>> l_bits(launches.size());
+    for (size_t l = 0; l < launches.size(); ++l) {
+      int b = 0;
+      for (int h : launches[l]) {
+        const int t = enc.live_max[h] - DENSE_LMAX;
+        l_base[l].push_back(b);
+        l_bits[l].push_back((int8_t)t);
+        l_hist[l].push_back(h);
+        for (int r = 0; r < (1 << t); ++r) l_wgteam[l].push_back((int32_t)l_base[l].size() - 1);
+        b += 1 << t;
+      }
+      max_wgs = std::max(max_wgs, l_wgteam[l].size());
+      max_teams = std::max(max_teams, l_base[l].size());
+    }
+    if (max_wgs) {
+      HIP_TRY(d_mirror.ensure((max_wgs << (DENSE_LMAX - 3)) * 8));
+      HIP_TRY(d_tflags.ensure(max_wgs * 8));
+      HIP_TRY(d_ctl.ensure(max_teams * dense_ctl_bytes()));
       HIP_TRY(d_abort.ensure(16));
-      HIP_TRY(hipMemsetAsync(d_ctl.p, 0, (size_t)teams * dense_ctl_bytes(), stream));
+      HIP_TRY(d_wgteam.ensure(max_wgs * 4));
+      HIP_TRY(d_tbase.ensure(max_teams * 4));
+      HIP_TRY(d_tbits.ensure(max_teams));
+      HIP_TRY(d_thist.ensure(max_teams * 4));
       HIP_TRY(hipMemsetAsync(d_abort.p, 0, 16, stream));
-      p.team_size = G;
-      p.gtab = d_gtab.as<uint64_t>();
-      p.ctl = d_ctl.p;
-      p.abort = d_abort.as<int32_t>();
     }
     HIP_TRY(hipEventRecord(ev0, stream));
-    HIP_TRY(hipEventRecord(ev_fork, stream));
-    if (nx) {
-      HIP_TRY(hipStreamWaitEvent(stream3, ev_fork, 0));
-      DenseParams q = p;
-      q.n = nx;
-      q.order = d_dorder.as<int32_t>() + nb + nw;
-      q.queue = d_dqueue.as<int32_t>() + 2;
-      HIP_TRY(launch_dense(q, DENSE_WIDE, teams * G, stream3));
-      HIP_TRY(hipEventRecord(ev_join2, stream3));
-    }
     if (nw) {
+      HIP_TRY(hipEventRecord(ev_fork, stream));
       HIP_TRY(hipStreamWaitEvent(stream2, ev_fork, 0));
       DenseParams q = p;
       q.n = nw;
@@ -393,25 +406,48 @@ struct lc_plan {
       HIP_TRY(launch_dense(q, DENSE_WAVE, std::min(dgrid_w, (nw + 3) / 4), stream2));
       HIP_TRY(hipEventRecord(ev_join, stream2));
     }
-    if (nb) {
+    for (size_t l = 0; l < launches.size(); ++l) {
+      const int nt = (int)l_base[l].size(), twgs = (int)l_wgteam[l].size();
       DenseParams q = p;
-      q.n = nb;
+      q.n = l == 0 ? nb : 0;
       q.order = d_dorder.as<int32_t>();
       q.queue = d_dqueue.as<int32_t>();
-      HIP_TRY(launch_dense(q, DENSE_BLOCK, std::min(dgrid_b, nb), stream));
+      q.n_team_wgs = twgs;
+      if (nt) {
+        HIP_TRY(hipMemcpyAsync(d_wgteam.p, l_wgteam[l].data(), twgs * 4, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(d_tbase.p, l_base[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(d_tbits.p, l_bits[l].data(), nt, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(d_thist.p, l_hist[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemsetAsync(d_tflags.p, 0, (size_t)twgs * 8, stream));
+        HIP_TRY(hipMemsetAsync(d_ctl.p, 0, (size_t)nt * dense_ctl_bytes(), stream));
+        q.wg_team = d_wgteam.as<int32_t>();
+        q.team_base = d_tbase.as<int32_t>();
+        q.team_bits = d_tbits.as<int8_t>();
+        q.team_hist = d_thist.as<int32_t>();
+        q.mirror = d_mirror.as<uint64_t>();
+        q.flags = d_tflags.as<unsigned long long>();
+        q.ctl = d_ctl.p;
+        q.abort = d_abort.as<int32_t>();
+        if (debug() && l == 0) {
+          HIP_TRY(d_tstamps.ensure((size_t)twgs * 64));
+          HIP_TRY(hipMemsetAsync(d_tstamps.p, 0, (size_t)twgs * 64, stream));
+          q.tstamps = d_tstamps.as<unsigned long long>();
+        }
+      }
+      const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n));
+      if (grid > 0) HIP_TRY(launch_dense(q, DENSE_BIG, grid, stream));
     }
     if (nw) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
-    if (nx) HIP_TRY(hipStreamWaitEvent(stream, ev_join2, 0));
     HIP_TRY(hipEventRecord(ev1, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     float t = 0;
     HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
     *ms += t;
-    if (nx) {
+    if (max_wgs) {
       int32_t ab = 0;
       HIP_TRY(hipMemcpy(&ab, d_abort.p, 4, hipMemcpyDeviceToHost));
       if (ab) {
-        last_error = "dense wide-team barrier watchdog fired (a team workgroup was not resident)";
+        last_error = "dense tile-team watchdog fired (a team workgroup was not resident)";
         return LC_E_INTERNAL;
       }
     }
@@ -424,16 +460,29 @@ struct lc_plan {
     HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
     for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x})
       for (int h : *ids) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
-    stats[1] += (nb ? 1 : 0) + (nw ? 1 : 0) + (nx ? 1 : 0);
+    stats[1] += (nw ? 1 : 0) + (double)launches.size();
     stats[12] += nb + nw + nx;
     stats[13] += t;
     stats[2] += (double)ss[SS_STEPS];
     stats[4] += (double)ss[SS_FOUT] + (nb + nw + nx);  // frontier in = previous frontier out (+ initial)
     stats[6] += (double)ss[SS_FOUT];
     if (debug()) {
-      fprintf(stderr, "[lincheck] dense: %d block + %d wave + %d wide (%d teams x %d) histories: %.3f ms, "
-              "steps=%llu Fout=%llu\n", nb, nw, nx, teams, G, t, ss[SS_STEPS], ss[SS_FOUT]);
+      fprintf(stderr, "[lincheck] dense: %d block + %d wave + %d tile-team histories (%zu launch(es), %zu team "
+              "workgroups): %.3f ms, steps=%llu Fout=%llu\n", nb, nw, nx, launches.size(), max_wgs, t,
+              ss[SS_STEPS], ss[SS_FOUT]);
       dense_report();
+      if (!launches[0].empty()) {  // phase split of the first tile team (the heaviest history)
+        const int g0 = 1 << l_bits[0][0];
+        std::vector<unsigned long long> TS((size_t)g0 * 8);
+        if (hipMemcpy(TS.data(), d_tstamps.p, TS.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
+          for (int r = 0; r < g0; ++r) {
+            const double st = std::max(1.0, (double)TS[r * 8 + 5]);
+            fprintf(stderr, "[lincheck]     tile team h=%d rank %2d: per team step us: wait %.1f compute %.1f "
+                    "publish %.1f return %.1f barrier %.1f (%.0f steps)\n", l_hist[0][0], r, TS[r * 8] / st / 100,
+                    TS[r * 8 + 1] / st / 100, TS[r * 8 + 2] / st / 100, TS[r * 8 + 3] / st / 100,
+                    TS[r * 8 + 4] / st / 100, st);
+          }
+      }
     }
     return 0;
   }
@@ -441,13 +490,13 @@ struct lc_plan {
   // LC_DEBUG: per-team spans and the slowest histories (s_memrealtime, 100 MHz)
   void dense_report() {
     const int n = enc.n_hist;
-    std::vector<unsigned long long> T((size_t)n * 2);
+    std::vector<unsigned long long> T((size_t)n * 4);
     if (hipMemcpy(T.data(), d_dstamps.p, T.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     const std::vector<int>* lists[3] = {&dense_b, &dense_w, &dense_x};
     const char* names[3] = {"block", "wave", "wide"};
     unsigned long long t0 = ~0ull;
     for (auto* ids : lists)
-      for (int h : *ids) t0 = std::min(t0, T[2 * h]);
+      for (int h : *ids) t0 = std::min(t0, T[4 * h]);
     for (int team = 0; team < 3; ++team) {
       const std::vector<int>& ids = *lists[team];
       if (ids.empty()) continue;
@@ -455,9 +504,9 @@ struct lc_plan {
       double by_l_us[64] = {0}, by_l_steps[64] = {0};
       std::vector<std::pair<double, int>> dur;
       for (int h : ids) {
-        first = std::min(first, T[2 * h]);
-        last = std::max(last, T[2 * h + 1]);
-        const double us = (double)(T[2 * h + 1] - T[2 * h]) / 100.0;
+        first = std::min(first, T[4 * h]);
+        last = std::max(last, T[4 * h + 1]);
+        const double us = (double)(T[4 * h + 1] - T[4 * h]) / 100.0;
         dur.push_back({us, h});
         by_l_us[enc.live_max[h]] += us;
         by_l_steps[enc.live_max[h]] += enc.n_steps(h);
@@ -467,8 +516,12 @@ struct lc_plan {
               (first - t0) / 100.0, (last - t0) / 100.0);
       for (int i = 0; i < (int)dur.size() && i < 4; ++i) {
         const int h = dur[i].second;
-        fprintf(stderr, "[lincheck]     slowest #%d: h=%d width=%d steps=%d %.1f us (start %.1f)\n", i, h,
-                enc.live_max[h], enc.n_steps(h), dur[i].first, (T[2 * h] - t0) / 100.0);
+        fprintf(stderr, "[lincheck]     slowest #%d: h=%d width=%d steps=%d %.1f us (start %.1f)", i, h,
+                enc.live_max[h], enc.n_steps(h), dur[i].first, (T[4 * h] - t0) / 100.0);
+        if (T[4 * h + 3])
+          fprintf(stderr, " team steps %llu: %.1f us (%.1f us each)", T[4 * h + 3], T[4 * h + 2] / 100.0,
+                  T[4 * h + 2] / 100.0 / (double)T[4 * h + 3]);
+        fprintf(stderr, "\n");
       }
       for (int l = 0; l < 64; ++l)
         if (by_l_steps[l] > 0)

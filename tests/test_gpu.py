@@ -304,21 +304,23 @@ def _wide_batch():
     return h, widths, _WIDE["exp"]
 
 
-@pytest.mark.parametrize("team", ["8x8", "2x1", "1x2"])
-def test_gpu_dense_wide_teams(team, monkeypatch):
-    """Wide teams: steps of width <= 17 on the leader's LDS table, wider steps on the team's
-    HBM table with one team barrier per layer. Team size and count must not change answers
-    (2x1: one two-workgroup team takes every history in turn; 1x2: leader-only teams)."""
-    g, teams = team.split("x")
-    monkeypatch.setenv("LC_WIDE_G", g)
-    monkeypatch.setenv("LC_WIDE_TEAMS", teams)
+@pytest.mark.parametrize("cap", [None, "8", "1"])
+def test_gpu_dense_tile_teams(cap, monkeypatch):
+    """Tile teams (width 18..22): 2^(width-17) workgroups, one 17-bit LDS tile each; cross-tile
+    pulls through HBM mirrors and per-layer tokens, team-slot returns through the mirrors.
+    Packing the teams into several launches (LC_TILE_WGS) must not change answers."""
+    if cap:
+        monkeypatch.setenv("LC_TILE_WGS", cap)
     h, widths, exp = _wide_batch()
     p = _lib.Plan(1, 0, h)
     p.run()
     got = p.results()
-    assert p.stats()["dense_histories"] == h.n_hist
+    s = p.stats()
+    assert s["dense_histories"] == h.n_hist
+    if cap == "1":
+        assert s["launches"] >= h.n_hist  # one launch per team
     for k in range(h.n_hist):
-        _cmp(got, exp[k], k, f"wide {team} w={widths[k]}")
+        _cmp(got, exp[k], k, f"tile cap={cap} w={widths[k]}")
     p.close()
 
 
