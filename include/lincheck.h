@@ -131,8 +131,11 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  *  8 config bytes (C)                                     9 algorithmic bytes
  * 10 workgroups                                          11 spill inserts
  * 12 histories decided by the dense closure-table kernels 13 dense kernels' ms (part of 0)
+ * 14 dense big kernel ms (its own stream)               15 dense wave kernel ms (its own stream)
+ * 16 dense big kernel algorithmic HBM bytes             17 dense big kernel algorithmic LDS bytes
+ * 18 dense wave kernel algorithmic HBM bytes            19 dense wave kernel algorithmic LDS bytes
  */
-#define LC_STATS_N 14
+#define LC_STATS_N 20
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
 void lc_plan_destroy(lc_plan* p);
 

@@ -109,23 +109,27 @@ struct HbmTab {
 // local hi bit below and the in-word closure. Returns popcount(R); *out = X | R.
 // opv: lane k holds slot k's decoded op (read with readlane, wave-uniform).
 template <int HMAX, int BATCH>
-__device__ __forceinline__ uint32_t close_word(uint64_t* B, uint32_t w, uint32_t live, int j, int H,
-                                              uint32_t opv, uint64_t R0, uint64_t* out) {
+__device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero, uint32_t w, uint32_t live, int j,
+                                              int H, uint32_t opv, uint64_t R0, uint64_t* out) {
   const uint64_t X = B[w];
   uint64_t R = R0;
   const bool j_lo = j < 3;
   const uint32_t jh = j_lo ? 0u : 1u << (j - 3);
   const bool has_j = (w & jh) != 0;
-  // ---- pulls from the finalized words one hi bit below. A rolled loop with the op read by
-  // a uniform-index readlane: unrolling it keeps a 64-bit uniform mask live per bit, which
-  // spills the SGPRs into VGPR lanes and costs more than the loads it would overlap.
-#pragma unroll 2
-  for (int b = 0; b < H; ++b) {
-    const uint32_t bit = 1u << b;
-    const bool act = has_j ? (bit == jh) : ((w & bit) != 0);
-    uint64_t v = 0;
-    if (act) v = B[w ^ bit];
-    R |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, b + 3), v, 0xffu, ~0ull, 0);
+  // ---- pulls from the finalized words one hi bit below, BATCH bits at a time: the loads of
+  // a batch are issued together (lanes without the bit read a zero word instead of taking a
+  // branch), then the batch's ops are applied. Bits >= H read the zero word (w < 2^H).
+  const uint32_t pm = has_j ? jh : w;  // bits this word pulls over
+  for (int b0 = 0; b0 < H; b0 += BATCH) {
+    uint64_t v[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const uint32_t bit = 1u << (b0 + u);
+      v[u] = *((pm & bit) ? &B[w ^ bit] : zero);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u)
+      R |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, b0 + u + 3), v[u], 0xffu, ~0ull, 0);
   }
   if (!has_j) {
     const uint32_t notj = j_lo ? keep8(j) : 0xffu;
@@ -154,7 +158,7 @@ __device__ __forceinline__ uint32_t close_word(uint64_t* B, uint32_t w, uint32_t
 // tt = 0..nt-1; sync() ends every layer (the last one too: the return that follows reads
 // the last layer's words).
 template <int HMAX, int BATCH, class Sync>
-__device__ __forceinline__ unsigned long long run_layers(uint64_t* B, const uint32_t* words, const uint32_t* wofs,
+__device__ __forceinline__ unsigned long long run_layers(uint64_t* B, const uint64_t* zero, const uint32_t* words, const uint32_t* wofs,
                                                         const uint32_t* binom, uint32_t live, int j,
                                                         uint32_t opv, int tt, int nt, Sync&& sync) {
   const int L = 32 - __clz((int)live);
@@ -163,12 +167,13 @@ __device__ __forceinline__ unsigned long long run_layers(uint64_t* B, const uint
   unsigned long long expl = 0;
   for (int q = 0; q <= H; ++q) {
     // words of popcount q below 2^H: a prefix of layer q of the sorted list
-    const uint32_t nq = binom[H * BINOM_N + q], o = wofs[q];
+    const uint32_t nq = __builtin_amdgcn_readfirstlane(binom[H * BINOM_N + q]);
+    const uint32_t o = __builtin_amdgcn_readfirstlane(wofs[q]);
     for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)nt) {
       const uint32_t w = words[o + r];
       if (w & ~live_hi) continue;
       uint64_t nv;
-      expl += close_word<HMAX, BATCH>(B, w, live, j, H, opv, 0ull, &nv);
+      expl += close_word<HMAX, BATCH>(B, zero, w, live, j, H, opv, 0ull, &nv);
     }
     sync();
   }
@@ -264,7 +269,7 @@ struct StreamWin {
 // decode the step header at pos; lanes < ninv of the calling wave store their op words
 __device__ __forceinline__ uint32_t read_step(const StreamWin& sw, int64_t pos, int lane, bool writer,
                                              uint32_t* opt, int* ninv_out) {
-  const uint32_t H0 = sw.at(pos);
+  const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sw.at(pos));  // wave-uniform
   const int ninv = (int)(H0 >> 27);
   const uint32_t w = sw.at(pos + 1 + lane);
   if (writer && lane < ninv) opt[w & 31u] = decode_op((w >> 8) & 0xffu, (w >> 16) & 0xffu);
@@ -275,7 +280,8 @@ __device__ __forceinline__ uint32_t read_step(const StreamWin& sw, int64_t pos, 
 // Histories dequeued one at a time by a team of TEAM threads (a wave or a workgroup) that
 // keeps the whole table in LDS (B, 2^(TLOG-3) words).
 template <int TEAM, int TLOG>
-__device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, uint32_t* opt, int* sQ,
+__device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, const uint64_t* zero, uint32_t* opt,
+                                             int* sQ,
                                              unsigned long long* sExpl, const uint32_t* words,
                                              const uint32_t* wofs, const uint32_t* binom, int tt,
                                              unsigned long long& st_fout, unsigned long long& st_steps) {
@@ -309,7 +315,25 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
       const uint32_t live = H0 & 0x3fffffu;
       const int j = (int)((H0 >> 22) & 31u);
       const uint32_t opv = opt[lane & 31];  // lane k: slot k's op, read with readlane
-      expl += run_layers<HMAX, 4>(B, words, wofs, binom, live, j, opv, tt, TEAM, [] { team_sync<TEAM>(); });
+      const int Lw = 32 - __clz((int)live);
+      const int nwt = 1 << (Lw > 3 ? Lw - 3 : 0);
+      unsigned long long t0 = 0, nzx = 0, e0 = expl;
+      if (p.lhist) {
+        for (int i = tt; i < nwt; i += TEAM) nzx += B[i] != 0;
+        t0 = __builtin_amdgcn_s_memrealtime();
+      }
+      expl += run_layers<HMAX, 4>(B, zero, words, wofs, binom, live, j, opv, tt, TEAM, [] { team_sync<TEAM>(); });
+      if (p.lhist) {
+        const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+        unsigned long long nza = 0;
+        for (int i = tt; i < nwt; i += TEAM) nza += B[i] != 0;
+        unsigned long long* lh = p.lhist + ((TEAM >= 256 ? 32 : 0) + Lw) * LH_N;
+        if (tt == 0) atomicAdd(&lh[0], 1ull), atomicAdd(&lh[1], dt);
+        if (nzx) atomicAdd(&lh[2], nzx);
+        if (nza) atomicAdd(&lh[3], nza);
+        if (expl - e0) atomicAdd(&lh[4], expl - e0);
+        team_sync<TEAM>();
+      }
       const uint64_t anyv = return_slot(B, live, j, tt, TEAM, st_fout);
       ++st_steps;
       if (!team_any<TEAM>(anyv != 0)) {
@@ -356,9 +380,11 @@ __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
   __shared__ uint32_t sBinom[BINOM_N * BINOM_N];
   __shared__ uint32_t sOp[NTEAM][32];
   __shared__ int sQ[NTEAM];
+  __shared__ uint64_t sZero;  // the word pulls of absent bits read
   __shared__ unsigned long long sExpl[NTEAM];
   const int tid = threadIdx.x, team = tid / 64, tt = tid % 64;
   init_tables(sBinom, sWOff, HMAX, WAVE_WG);
+  if (tid == 0) sZero = 0;
   for (int v = tid; v < (1 << HMAX); v += WAVE_WG) {  // colex rank within its popcount layer
     uint32_t rank = 0;
     int i = 0;
@@ -367,7 +393,7 @@ __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
   }
   __syncthreads();
   unsigned long long st_fout = 0, st_steps = 0;
-  history_loop<64, DENSE_WAVE_LMAX>(p, &sTab[team << HMAX], sOp[team], &sQ[team], &sExpl[team], sWords, sWOff,
+  history_loop<64, DENSE_WAVE_LMAX>(p, &sTab[team << HMAX], &sZero, sOp[team], &sQ[team], &sExpl[team], sWords, sWOff,
                                     sBinom, tt, st_fout, st_steps);
   flush_stats(p, st_fout, st_steps, tt == 0);
 }
@@ -470,15 +496,16 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   __shared__ long long sPos;
   __shared__ unsigned sAny;
   __shared__ unsigned long long sRed;
+  __shared__ uint64_t sZero;
 
   const int tid = threadIdx.x, lane = tid & 63;
   init_tables(sBinom, sWOff, DENSE_WORD_BITS, 1024);
-  if (tid == 0) sAbort = 0;
+  if (tid == 0) sAbort = 0, sZero = 0;
   __syncthreads();
   unsigned long long st_fout = 0, st_steps = 0;
 
   if ((int)blockIdx.x >= p.n_team_wgs) {  // ------------------------------- BLOCK histories
-    history_loop<1024, DENSE_LMAX>(p, sTab, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout, st_steps);
+    history_loop<1024, DENSE_LMAX>(p, sTab, &sZero, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout, st_steps);
     flush_stats(p, st_fout, st_steps, tid == 0);
     return;
   }
@@ -506,7 +533,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   auto team_step = [&](long long hpos) -> bool {
     ++stepctr;
     const unsigned long long tok0 = stepctr << 5;
-    const uint32_t H0 = p.stream[hpos];
+    const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.stream[hpos]);
     const uint32_t live = H0 & 0x3fffffu;
     const int j = (int)((H0 >> 22) & 31u);
     const uint32_t opv = sOp[lane & 31];
@@ -552,9 +579,9 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
             if (R0) sTab[w] = nv;
             expl += (uint32_t)__popcll(R0);
           } else {
-            expl += close_word<HSOLO, 4>(sTab, w, live_loc, j, H, opv, R0, &nv);
+            expl += close_word<HSOLO, 4>(sTab, &sZero, w, live_loc, j, H, opv, R0, &nv);
           }
-          if (!(p.dbg & 1)) HbmTab::st(mine + mo + r, nv);  // mirrors are in word-list order
+          HbmTab::st(mine + mo + r, nv);  // mirrors are in word-list order
         }
         mo += nq;
         __syncthreads();
@@ -620,7 +647,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
       bool survived;
       if ((live >> DENSE_LMAX) == 0) {  // narrow step: the leader alone (other tiles empty)
         const uint32_t opv = sOp[lane & 31];
-        expl += run_layers<HSOLO, 4>(sTab, p.words, sWOff, sBinom, live, j, opv, tid, 1024,
+        expl += run_layers<HSOLO, 4>(sTab, &sZero, p.words, sWOff, sBinom, live, j, opv, tid, 1024,
                                      [] { __syncthreads(); });
         survived = __syncthreads_or(return_slot(sTab, live, j, tid, 1024, st_fout) != 0);
       } else {  // wide step: every tile

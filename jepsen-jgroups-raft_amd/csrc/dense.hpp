@@ -53,13 +53,16 @@ struct DenseParams {
   void* ctl;                    // [teams] TeamCtl (zeroed before launch)
   int32_t* abort;               // set when a team barrier / token wait times out
   unsigned long long* tstamps;  // [n_team_wgs][8] LC_DEBUG phase cycles of each tile workgroup
-  int32_t dbg;                  // LC_DENSE_DBG experiment bits (timing only; 0 in production)
+  unsigned long long* lhist;    // LC_DEBUG [2 teams (wave, block)][32 widths][LH_N]; may be null
 };
 
 // Kernels: WAVE = 256-thread workgroups, one history per wave (width <= DENSE_WAVE_LMAX);
 // BIG = 1024-thread workgroups: tile teams (one history of width 18..DENSE_WIDE_LMAX each,
 // one workgroup per 17-bit LDS tile) and BLOCK histories (width <= DENSE_LMAX, one
 // workgroup each, LDS table) in the same launch.
+// LC_DEBUG per-width step profile: steps, step time (100 MHz), nonzero words before the
+// closure, nonzero words after it, configs explored
+constexpr int LH_N = 5;
 enum DenseTeam { DENSE_WAVE = 0, DENSE_BIG = 1 };
 hipError_t launch_dense(const DenseParams& p, DenseTeam kind, int grid, hipStream_t stream);
 int dense_grid_size(DenseTeam kind);

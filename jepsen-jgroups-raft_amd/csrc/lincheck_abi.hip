@@ -128,12 +128,16 @@ struct lc_plan {
   // dense closure tables (narrow cas-register histories; dense.hpp)
   std::vector<int> dense_b, dense_w, dense_x;  // block / wave / wide teams, heaviest first
   DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dwords, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
-  DevArray d_dstamps, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_thist;
+  DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_thist;
+  struct StepBytes { double lds, hbm; };
+  std::vector<StepBytes> dalg;     // per dense step: algorithmic bytes
+  std::vector<int64_t> dalg_off;    // [n_hist + 1] first step of each history in dalg
   int64_t dstream_words = 0;
   int dgrid_b = 0, dgrid_w = 0;
   int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_w0 = nullptr, ev_w1 = nullptr;  // per dense kernel
   bool spill_clean = false, kspill_clean = false;
   // results
   std::vector<int32_t> status, fail_step;
@@ -150,6 +154,8 @@ struct lc_plan {
     if (ev1) hipEventDestroy(ev1);
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_join) hipEventDestroy(ev_join);
+    for (hipEvent_t e : {ev_b0, ev_b1, ev_w0, ev_w1})
+      if (e) hipEventDestroy(e);
     if (stream2) hipStreamDestroy(stream2);
     if (stream) hipStreamDestroy(stream);
   }
@@ -202,6 +208,8 @@ struct lc_plan {
     if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
     if (!ev_fork) HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     if (!ev_join) HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    for (hipEvent_t* e : {&ev_b0, &ev_b1, &ev_w0, &ev_w1})
+      if (!*e) HIP_TRY(hipEventCreate(e));
     nwg = search_grid_size(model);
     dgrid_b = dense_grid_size(DENSE_BIG);
     dgrid_w = dense_grid_size(DENSE_WAVE);
@@ -261,6 +269,26 @@ struct lc_plan {
     return build_dense();
   }
 
+  // Algorithmic bytes of one dense step of width L with ninv invocations:
+  // LDS: W = 2^(L-3) words; the closure reads every word (8W) and its pulls (8 * H * W / 2),
+  // writes every word (8W), the return reads half and writes all (12W). HBM: the step's
+  // stream words; a tile-team step (L > 17) also writes every tile word to its mirror once and
+  // reads each cross-tile predecessor (t/2 per word on average) and the return's half.
+  static StepBytes step_alg_bytes(int L, int ninv) {
+    const int H = L > 3 ? L - 3 : 0;
+    const double W = std::ldexp(1.0, H);
+    StepBytes b{8.0 * W * (3.5 + 0.5 * H), 4.0 * (1 + ninv)};
+    if (L > DENSE_LMAX) b.hbm += 8.0 * W * (1.0 + 0.5 * (L - DENSE_LMAX) + 0.5);
+    return b;
+  }
+  // bytes of the steps history h ran (all of them, or up to its failing step)
+  StepBytes dense_hist_bytes(int h, int fail_t) const {
+    StepBytes b{0, 0};
+    const int64_t e = fail_t >= 0 ? std::min(dalg_off[h] + fail_t + 1, dalg_off[h + 1]) : dalg_off[h + 1];
+    for (int64_t i = dalg_off[h]; i < e; ++i) b.lds += dalg[i].lds, b.hbm += dalg[i].hbm;
+    return b;
+  }
+
   // Step streams for the dense closure-table kernels (format: dense.hpp). Eligible:
   // cas-register, <= DENSE_MAX_STATES register values, live width <= dense_maxw.
   int build_dense() {
@@ -274,7 +302,10 @@ struct lc_plan {
     std::vector<int32_t> nst(n, 0);
     std::vector<int8_t> lm(n, 0);
     std::vector<double> cost(n, 0.0);
+    dalg_off.assign(n + 1, 0);
+    dalg.clear();
     for (int h = 0; h < n; ++h) {
+      dalg_off[h] = (int64_t)dalg.size();
       if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || enc.live_max[h] > dense_maxw) continue;
       sbeg[h] = (int64_t)words.size();
       nst[h] = enc.n_steps(h);
@@ -295,6 +326,7 @@ struct lc_plan {
         }
         const int L = 32 - __builtin_clz(live);
         cost[h] += (double)(1u << L) * L;
+        dalg.push_back(step_alg_bytes(L, (int)(q1 - q0)));
       }
       const int lw = enc.live_max[h];
       (lw <= DENSE_WAVE_LMAX ? dense_w : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
@@ -306,6 +338,7 @@ struct lc_plan {
     std::vector<int32_t> ord(dense_b.begin(), dense_b.end());
     ord.insert(ord.end(), dense_w.begin(), dense_w.end());
     ord.insert(ord.end(), dense_x.begin(), dense_x.end());
+    dalg_off[n] = (int64_t)dalg.size();
     dstream_words = (int64_t)words.size();
     int rc;
     if ((rc = upload(d_dstream, words))) return rc;
@@ -348,11 +381,13 @@ struct lc_plan {
     p.explored = d_dexpl.as<unsigned long long>();
     p.stats = d_stats.as<unsigned long long>();
     p.stamps = nullptr;
-    if (const char* e = getenv("LC_DENSE_DBG")) p.dbg = atoi(e);
     if (debug()) {
       HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
       HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
       p.stamps = d_dstamps.as<unsigned long long>();
+      HIP_TRY(d_dlhist.ensure(64 * LH_N * 8));
+      HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, 64 * LH_N * 8, stream));
+      p.lhist = d_dlhist.as<unsigned long long>();
     }
     // tile teams: one per wide history, 2^(width - 17) workgroups; packed into launches of at
     // most `cap` workgroups (the first launch also runs the BLOCK histories)
@@ -403,9 +438,12 @@ struct lc_plan {
       q.n = nw;
       q.order = d_dorder.as<int32_t>() + nb;
       q.queue = d_dqueue.as<int32_t>() + 1;
+      HIP_TRY(hipEventRecord(ev_w0, stream2));
       HIP_TRY(launch_dense(q, DENSE_WAVE, std::min(dgrid_w, (nw + 3) / 4), stream2));
+      HIP_TRY(hipEventRecord(ev_w1, stream2));
       HIP_TRY(hipEventRecord(ev_join, stream2));
     }
+    HIP_TRY(hipEventRecord(ev_b0, stream));
     for (size_t l = 0; l < launches.size(); ++l) {
       const int nt = (int)l_base[l].size(), twgs = (int)l_wgteam[l].size();
       DenseParams q = p;
@@ -437,6 +475,7 @@ struct lc_plan {
       const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n));
       if (grid > 0) HIP_TRY(launch_dense(q, DENSE_BIG, grid, stream));
     }
+    HIP_TRY(hipEventRecord(ev_b1, stream));
     if (nw) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
     HIP_TRY(hipEventRecord(ev1, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -463,6 +502,20 @@ struct lc_plan {
     stats[1] += (nw ? 1 : 0) + (double)launches.size();
     stats[12] += nb + nw + nx;
     stats[13] += t;
+    // per-kernel time (events on each kernel's own stream) and algorithmic bytes of the steps
+    // each kernel ran: 14/15 big/wave ms, 16/17 big HBM/LDS bytes, 18/19 wave HBM/LDS bytes
+    float tb = 0, tw = 0;
+    HIP_TRY(hipEventElapsedTime(&tb, ev_b0, ev_b1));
+    if (nw) HIP_TRY(hipEventElapsedTime(&tw, ev_w0, ev_w1));
+    stats[14] += tb;
+    stats[15] += tw;
+    for (const std::vector<int>* ids : {&dense_b, &dense_x, &dense_w})
+      for (int h : *ids) {
+        const StepBytes b = dense_hist_bytes(h, fs[h]);
+        const int k = ids == &dense_w ? 18 : 16;
+        stats[k] += b.hbm;
+        stats[k + 1] += b.lds;
+      }
     stats[2] += (double)ss[SS_STEPS];
     stats[4] += (double)ss[SS_FOUT] + (nb + nw + nx);  // frontier in = previous frontier out (+ initial)
     stats[6] += (double)ss[SS_FOUT];
@@ -471,6 +524,17 @@ struct lc_plan {
               "workgroups): %.3f ms, steps=%llu Fout=%llu\n", nb, nw, nx, launches.size(), max_wgs, t,
               ss[SS_STEPS], ss[SS_FOUT]);
       dense_report();
+      std::vector<unsigned long long> LH(64 * LH_N);
+      if (hipMemcpy(LH.data(), d_dlhist.p, LH.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
+        for (int k = 0; k < 64; ++k) {
+          const unsigned long long* e = &LH[k * LH_N];
+          if (!e[0]) continue;
+          const int L = k & 31;
+          const double s = (double)e[0];
+          fprintf(stderr, "[lincheck]   %s step width %2d: %8llu steps %7.2f us/step  nonzero words %8.1f -> %8.1f "
+                  "of %d  explored %8.1f\n", k >= 32 ? "block" : "wave ", L, e[0], e[1] / s / 100.0, e[2] / s,
+                  e[3] / s, 1 << (L > 3 ? L - 3 : 0), e[4] / s);
+        }
       if (!launches[0].empty()) {  // phase split of the first tile team (the heaviest history)
         const int g0 = 1 << l_bits[0][0];
         std::vector<unsigned long long> TS((size_t)g0 * 8);

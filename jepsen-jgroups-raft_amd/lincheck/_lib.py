@@ -15,10 +15,12 @@ LIB_PATH = os.path.join(HERE, "liblincheck.so")
 EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_failure_configs",
            "lc_counter_bounds", "lc_plan_create", "lc_plan_run", "lc_plan_results",
            "lc_plan_stats", "lc_plan_destroy")
-STATS_N = 14
+STATS_N = 20
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
-               "spill_inserts", "dense_histories", "dense_ms")
+               "spill_inserts", "dense_histories", "dense_ms", "dense_big_ms", "dense_wave_ms",
+               "dense_big_hbm_bytes", "dense_big_lds_bytes", "dense_wave_hbm_bytes",
+               "dense_wave_lds_bytes")
 
 P = C.c_void_p
 I8P = C.POINTER(C.c_int8)

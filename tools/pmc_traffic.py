@@ -16,7 +16,7 @@ def per_dispatch(path, kernel, counter):
     return vals
 
 
-def main(tag, fetch_csv, write_csv, workload, scale, kernel="search_kernel"):
+def main(tag, fetch_csv, write_csv, workload, scale, kernel="dense_big_kernel"):
     f = per_dispatch(fetch_csv, kernel, "FETCH_SIZE")
     w = per_dispatch(write_csv, kernel, "WRITE_SIZE")
     fb = sum(f) / len(f) * 1024

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Runs on the GPU box: bench line + rocprofv3 kernel trace/stats + PMC traffic passes.
+# Runs on the GPU box: bench line + rocprofv3 kernel trace/stats + PMC passes (HBM traffic,
+# then vector/scalar/LDS instruction counts), each pass a run of its own.
 # usage: tools/profile_round.sh <tag> [bench args...]
 set -o pipefail
 tag=$1; shift
@@ -13,4 +14,7 @@ timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_f
   python -u bench.py "$@" --no-cpu --steps 1 --warmup 0 > $out/pmc_fetch.log 2>&1 || exit 1
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run -- \
   python -u bench.py "$@" --no-cpu --steps 1 --warmup 0 > $out/pmc_write.log 2>&1 || exit 1
+timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES \
+  SQ_WAVE_CYCLES --output-format csv -d $out/pmc_sq -o run -- \
+  python -u bench.py "$@" --no-cpu --steps 1 --warmup 0 > $out/pmc_sq.log 2>&1 || exit 1
 echo done
