@@ -75,6 +75,107 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int):
              "configs_per_s": sum(r["explored"] for r in res) / wall}, res, sample, hs)
 
 
+def bench_c5(args, rank, world, dist, barrier_sync):
+    """C5: the counter bounds scan (BASELINE configs[4]) over one 1M-op history. The history's
+    entries are split over the ranks (strong scaling); each step is ONE exchange of five int64
+    sums per rank (all-gather over RCCL) + the rank's scan + an all-reduce MIN of the verdict
+    (SURVEY §8(e) axis 3). Inputs are HBM-resident (lc_bounds_plan)."""
+    from lincheck import shard
+    tdist = dist[1] if dist else None
+    h = synth.gen_config("c5", scale=args.scale)
+    n = int(h.off[1] - h.off[0])
+    own = shard.bounds_shard(n, rank, world)
+    t0 = time.perf_counter()
+    plan = _lib.BoundsPlan(0, h, own=own, device=int(os.environ.get("LOCAL_RANK", 0)))
+    log(f"[rank {rank}] c5: {n} entries, {h.n_ops()} ops, shard {own}; "
+        f"plan {time.perf_counter() - t0:.2f}s")
+
+    def step():
+        excl = shard.exclusive_sums(plan.sums(), tdist) if world > 1 else None
+        ok, bad, ms = plan.run(excl)
+        return shard.first_bad(bad, tdist), ms
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync()
+    kms = 0.0
+    bad = -1
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bad, ms = step()
+        kms += ms
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        torch, td = dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        td.all_reduce(t, op=td.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        plan.close()
+        return None
+    # algorithmic HBM bytes of rank 0's scan per step (DESIGN.md §3.3): the two delta arrays
+    # read by the reduce (16 B/entry) and by the prefix pass (16 B + the 4-B observation map),
+    # per observation its five prefixes written (40 B) and read back with its record (40 + 32
+    # B); plus the block-sum pass before the exchange when sharded (16 B/entry)
+    n_own = own[1] - own[0]
+    is_obs = (h.type == 1) & (((h.f == 0) & (h.vflags == 1)) |
+                              (((h.f == 5) | (h.f == 6)) & (h.vflags == 2)))
+    n_obs = int(is_obs[own[0]:own[1]].sum())
+    alg = 36 * n_own + 112 * n_obs + (16 * n_own if world > 1 else 0)
+    k_s = kms / args.steps / 1e3
+    achieved = alg / k_s / 1e9 if k_s > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tr = json.load(open(args.traffic))
+            if tr.get("workload") == "c5" and abs(tr.get("scale", 1.0) - args.scale) < 1e-9:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+    cpu = None
+    if not args.no_cpu and world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # noqa: E402  (bench cpu_baseline leg only)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            eok, ebad = oracle.counter_bounds(h)
+            reps += 1
+            if time.perf_counter() - t0 > min(args.cpu_budget, 10.0):
+                break
+        wall = (time.perf_counter() - t0) / reps
+        cpu = {"value": h.n_ops() / wall, "unit": "history ops/s", "cores": 1, "kind": "port",
+               "sample": f"the whole {h.n_ops()}-op history, {reps} scan(s), 1 thread",
+               "wall_s": round(wall, 4),
+               "parity": {"ok": bool(eok) == (bad < 0), "bad_idx": int(ebad) == bad}}
+    out = {
+        "metric": "history ops verified/sec (+ configs explored/sec, % HBM roofline)",
+        "value": h.n_ops() * args.steps / elapsed,
+        "unit": "history ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (simulated linearizable counter SUT, SURVEY §8(d) seeds)",
+        "config": {"workload": "c5: counter 1M ops, 16 clients, p_info 0.01: bounds prefix scan",
+                   "ops": h.n_ops(), "entries": n, "scale": args.scale,
+                   "parallelism": f"entries split over {world} GPU(s), one 5 x int64 all-gather "
+                                  "per step"},
+        "verdict": {"bounds_ok": bad < 0, "bad_idx": bad},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "lc::bounds_{reduce,scan_partials,prefix,check}",
+                     "kernel_ms": k_s * 1e3, "alg_bytes_per_launch": alg},
+        "cpu_baseline": cpu,
+    }
+    plan.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +205,14 @@ def main():
             dist[0].cuda.synchronize()
             dist[1].barrier()
             dist[0].cuda.synchronize()
+
+    if args.workload == "c5":
+        out = bench_c5(args, rank, world, dist, barrier_sync)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist[1].destroy_process_group()
+        return
 
     model = MODEL_OF[args.workload]
     kind = _lib.MODEL_KIND[model]

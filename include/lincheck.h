@@ -107,6 +107,26 @@ int32_t lc_counter_bounds(int64_t init_value, int32_t n_hist, const int64_t* his
                           const int8_t* vflags, int8_t* out_ok, int64_t* out_bad_idx,
                           char* err, int32_t err_len);
 
+/* ---- device-resident counter bounds plans (the C5 bounds scan on HBM-resident inputs) ----
+ * One counter history, or one shard of it: the plan owns the observations (reads, *-and-get)
+ * completed in entries [own_begin, own_end) and keeps those entries plus the halo back to the
+ * earliest owned observation's invocation in HBM. Sharded use (SURVEY §8(e) axis 3): every
+ * shard calls lc_bounds_plan_sums (five sums over its owned entries), the shards exchange them
+ * (one all-gather of 5 x int64 per shard), and each runs with the sums of all entries before
+ * its own_begin. Unsharded: own = [0, n), excl_sums = NULL. out_bad_idx = :index of the first
+ * owned completion proven out of bounds (-1 if none); a pass proves nothing (sound rejection).
+ * A plan is used by one thread at a time. */
+typedef struct lc_bounds_plan lc_bounds_plan;
+int32_t lc_bounds_plan_create(int32_t device, int64_t init_value, int64_t n, const int64_t* index,
+                              const int32_t* process, const int8_t* type, const int8_t* f,
+                              const int64_t* v0, const int64_t* v1, const int8_t* vflags,
+                              int64_t own_begin, int64_t own_end, lc_bounds_plan** out, char* err,
+                              int32_t err_len);
+int32_t lc_bounds_plan_sums(lc_bounds_plan* p, int64_t* out_sums /*[5]*/, char* err, int32_t err_len);
+int32_t lc_bounds_plan_run(lc_bounds_plan* p, const int64_t* excl_sums /*[5] or NULL*/, int8_t* out_ok,
+                           int64_t* out_bad_idx, double* out_ms, char* err, int32_t err_len);
+void lc_bounds_plan_destroy(lc_bounds_plan* p);
+
 /* ---- device-resident plans (benchmarking / repeated runs on HBM-resident inputs) ---- */
 typedef struct lc_plan lc_plan;
 

@@ -269,16 +269,21 @@ struct lc_plan {
     return build_dense();
   }
 
-  // Algorithmic bytes of one dense step of width L with ninv invocations:
-  // LDS: W = 2^(L-3) words; the closure reads every word (8W) and its pulls (8 * H * W / 2),
-  // writes every word (8W), the return reads half and writes all (12W). HBM: the step's
-  // stream words; a tile-team step (L > 17) also writes every tile word to its mirror once and
-  // reads each cross-tile predecessor (t/2 per word on average) and the return's half.
-  static StepBytes step_alg_bytes(int L, int ninv) {
+  // Algorithmic bytes of one dense step with live slots `live` and ninv invocations
+  // (DESIGN.md §3.4). LDS: the closure visits the words w over live hi slots (We =
+  // 2^popcount(live >> 3)), reading each (8 B) and its pulls (8 B per set bit: He / 2 on
+  // average) and writing it; the return reads half the table's 2^H words and writes all.
+  // HBM: the step's stream words; a tile-team step (slots >= 17 live) also writes every
+  // visited word to its tile's mirror once and reads each cross-tile predecessor (te / 2 per
+  // word on average, te live team slots) plus the return's half.
+  static StepBytes step_alg_bytes(uint32_t live, int ninv) {
+    const int L = 32 - __builtin_clz(live);
     const int H = L > 3 ? L - 3 : 0;
-    const double W = std::ldexp(1.0, H);
-    StepBytes b{8.0 * W * (3.5 + 0.5 * H), 4.0 * (1 + ninv)};
-    if (L > DENSE_LMAX) b.hbm += 8.0 * W * (1.0 + 0.5 * (L - DENSE_LMAX) + 0.5);
+    const int He = __builtin_popcount(live >> 3);
+    const double W = std::ldexp(1.0, H), We = std::ldexp(1.0, He);
+    StepBytes b{8.0 * We * (2.0 + 0.5 * He) + 12.0 * W, 4.0 * (1 + ninv)};
+    const int te = __builtin_popcount(live >> DENSE_LMAX);
+    if (te) b.hbm += 8.0 * We * (1.0 + 0.5 * te + 0.5);
     return b;
   }
   // bytes of the steps history h ran (all of them, or up to its failing step)
@@ -326,7 +331,7 @@ struct lc_plan {
         }
         const int L = 32 - __builtin_clz(live);
         cost[h] += (double)(1u << L) * L;
-        dalg.push_back(step_alg_bytes(L, (int)(q1 - q0)));
+        dalg.push_back(step_alg_bytes(live, (int)(q1 - q0)));
       }
       const int lw = enc.live_max[h];
       (lw <= DENSE_WAVE_LMAX ? dense_w : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(HERE, "liblincheck.so")
 # every symbol include/lincheck.h declares (tests check the exports)
 EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_failure_configs",
            "lc_counter_bounds", "lc_plan_create", "lc_plan_run", "lc_plan_results",
-           "lc_plan_stats", "lc_plan_destroy")
+           "lc_plan_stats", "lc_plan_destroy", "lc_bounds_plan_create", "lc_bounds_plan_sums",
+           "lc_bounds_plan_run", "lc_bounds_plan_destroy")
 STATS_N = 20
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
@@ -59,6 +60,15 @@ def load():
     L.lc_plan_stats.restype = C.c_int32
     L.lc_plan_destroy.argtypes = [P]
     L.lc_plan_destroy.restype = None
+    L.lc_bounds_plan_create.argtypes = [C.c_int32, C.c_int64, C.c_int64] + [P] * 7 + \
+        [C.c_int64, C.c_int64, C.POINTER(C.c_void_p), C.c_char_p, C.c_int32]
+    L.lc_bounds_plan_create.restype = C.c_int32
+    L.lc_bounds_plan_sums.argtypes = [P, P, C.c_char_p, C.c_int32]
+    L.lc_bounds_plan_sums.restype = C.c_int32
+    L.lc_bounds_plan_run.argtypes = [P] * 5 + [C.c_char_p, C.c_int32]
+    L.lc_bounds_plan_run.restype = C.c_int32
+    L.lc_bounds_plan_destroy.argtypes = [P]
+    L.lc_bounds_plan_destroy.restype = None
     if L.lc_abi_version() != 1:
         raise LincheckError("ABI version mismatch")
     _lib = L
@@ -167,6 +177,58 @@ class Plan:
     def close(self):
         if self._h:
             self._L.lc_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BoundsPlan:
+    """Device-resident counter bounds scan over one history, or over the shard of it whose
+    observations complete in entries [own_begin, own_end) (lc_bounds_plan_*). Sharded use:
+    sums() on every shard, exchange (lincheck.shard.exclusive_sums), then run(excl)."""
+
+    def __init__(self, init_value: int, h, hist: int = 0, own=None, device: int = 0):
+        L = load()
+        self._L = L
+        b, e = int(h.off[hist]), int(h.off[hist + 1])
+        n = e - b
+        own_begin, own_end = own if own is not None else (0, n)
+        self.own = (own_begin, own_end)
+        sl = slice(b, e)
+        self._keep = [np.ascontiguousarray(a[sl]) for a in
+                      (h.index, h.process, h.type, h.f, h.v0, h.v1, h.vflags)]
+        handle = C.c_void_p()
+        buf = _errbuf()
+        rc = L.lc_bounds_plan_create(device, init_value, n, *[_p(a) for a in self._keep], own_begin,
+                                     own_end, C.byref(handle), buf, len(buf))
+        _raise(rc, buf, "lc_bounds_plan_create")
+        self._h = handle
+        self._keep = None
+
+    def sums(self):
+        out = np.zeros(5, np.int64)
+        buf = _errbuf()
+        _raise(self._L.lc_bounds_plan_sums(self._h, _p(out), buf, len(buf)), buf, "lc_bounds_plan_sums")
+        return out
+
+    def run(self, excl=None):
+        """-> (ok, bad :index or -1, kernel ms)"""
+        ok = np.zeros(1, np.int8)
+        bad = np.zeros(1, np.int64)
+        ms = np.zeros(1, np.float64)
+        ex = None if excl is None else np.ascontiguousarray(excl, dtype=np.int64)
+        buf = _errbuf()
+        rc = self._L.lc_bounds_plan_run(self._h, _p(ex), _p(ok), _p(bad), _p(ms), buf, len(buf))
+        _raise(rc, buf, "lc_bounds_plan_run")
+        return bool(ok[0]), int(bad[0]), float(ms[0])
+
+    def close(self):
+        if self._h:
+            self._L.lc_bounds_plan_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -1,0 +1,68 @@
+"""Multi-rank paths on the CPU (torch.distributed gloo, world sizes 2 and 3, 127.0.0.1): the
+counter bounds scan's exclusive-prefix exchange and verdict reduction (SURVEY §8(e) axis 3)
+and the key/entry sharding the bench uses. The device half of a shard runs in test_gpu.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as tdist
+import torch.multiprocessing as mp
+
+from lincheck import shard
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, sums_all, bads, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        excl = shard.exclusive_sums(sums_all[rank], tdist)
+        fb = shard.first_bad(bads[rank], tdist)
+        q.put((rank, excl.tolist(), fb))
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exclusive_sums_and_first_bad_gloo(world):
+    rng = np.random.default_rng(world)
+    sums_all = [rng.integers(-1000, 1000, 5).astype(np.int64) for _ in range(world)]
+    bads = [-1] * world
+    bads[world - 1] = 77
+    if world > 2:
+        bads[1] = 12
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sums_all, bads, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (e, fb)) for r, e, fb in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        exp = np.sum(sums_all[:r], axis=0) if r else np.zeros(5, np.int64)
+        assert got[r][0] == exp.tolist()
+        assert got[r][1] == (12 if world > 2 else 77)
+
+
+def test_exchange_identity_without_process_group():
+    assert shard.exclusive_sums([1, 2, 3, 4, 5]).tolist() == [0] * 5
+    assert shard.first_bad(-1) == -1 and shard.first_bad(9) == 9
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (5, 3), (10, 4), (2_000_000, 8), (7, 8)])
+def test_shards_partition(n, world):
+    spans = [shard.bounds_shard(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (b0, e0), (b1, e1) in zip(spans, spans[1:]):
+        assert e0 == b1 and b0 <= e0
+    sizes = [e - b for b, e in spans]
+    assert max(sizes) - min(sizes) <= 1

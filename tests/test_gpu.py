@@ -151,6 +151,57 @@ def test_gpu_counter_bounds_c5_full_size():
     assert not ok[0] and not eok and int(bad[0]) == ebad
 
 
+def _sharded_bounds(h, world):
+    """Scan one counter history as `world` shards on one GPU: every shard's block sums, the
+    exclusive prefix an all-gather would give each, then each shard's run (lincheck.shard)."""
+    from lincheck import shard
+    n = int(h.off[1] - h.off[0])
+    plans = [_lib.BoundsPlan(0, h, own=shard.bounds_shard(n, r, world)) for r in range(world)]
+    sums = [p.sums() for p in plans]
+    bad = -1
+    try:
+        for r, p in enumerate(plans):
+            excl = np.sum(sums[:r], axis=0) if r else np.zeros(5, np.int64)
+            ok, b, ms = p.run(excl)
+            assert ok == (b < 0) and ms >= 0
+            if b >= 0 and (bad < 0 or b < bad):
+                bad = b
+    finally:
+        for p in plans:
+            p.close()
+    return bad < 0, bad
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+def test_gpu_bounds_plan_shards_vs_oracle(world):
+    for t in range(24):
+        h = synth.gen_counter(400, 5, 0.05, 900 + t, invalid=(t % 2 == 0))
+        ok, bad = _sharded_bounds(h, world)
+        eok, ebad = oracle.counter_bounds(h)
+        assert ok == eok and bad == ebad, (world, t)
+
+
+def test_gpu_bounds_plan_c5_full_size_sharded():
+    h = synth.gen_config("c5")
+    reads = np.nonzero((h.type == 1) & (h.f == 0))[0]
+    for world in (1, 8):
+        assert _sharded_bounds(h, world) == (True, -1)
+    j = reads[(3 * len(reads)) // 4]
+    h.v0[j] += 10 ** 6
+    eok, ebad = oracle.counter_bounds(h)
+    assert not eok
+    for world in (1, 8):
+        assert _sharded_bounds(h, world) == (False, ebad)
+
+
+def test_gpu_bounds_plan_empty_and_tiny():
+    for ev in ([], [{"process": 0, "type": "invoke", "f": "read", "value": None},
+                    {"process": 0, "type": "ok", "f": "read", "value": 3}]):
+        h = H.encode(ev)
+        eok, ebad = oracle.counter_bounds(h)
+        assert _sharded_bounds(h, 1) == (eok, ebad)
+
+
 def test_gpu_errors_are_unknown():
     bad = H.encode([{"process": 0, "type": "ok", "f": "read", "value": 1}])
     g = _lib.check(1, 0, bad)
