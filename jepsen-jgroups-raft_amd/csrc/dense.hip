@@ -52,23 +52,47 @@ struct TeamCtl {
   long long pos;
   unsigned any;
   unsigned pad2[27];
-  unsigned ops[32];
+  unsigned ops[64];  // the leader's op table (OpSel lo, hi per slot)
 };
 
-// decoded op, laid out for transfer(): srcsh[0:7) = 8 * source state, or OPF_FOLD (a write
-// reads every state); dstsh[8:14) = 8 * destination state; OPF_IDENT (read nil: every state
-// stays); OPF_NONE (the op names a value the register never holds: it moves nothing)
-constexpr uint32_t OPF_FOLD = 64u, OPF_IDENT = 1u << 16, OPF_NONE = 1u << 17;
-__device__ __forceinline__ uint32_t decode_op(uint32_t am, uint32_t bm) {
-  if (am == 0) return OPF_NONE;  // precondition names a value the register never holds
+// A decoded op is a byte permutation of the word's 8 state bytes: `lo`/`hi` are the
+// v_perm_b32 selectors of the result's low and high dwords (selector byte 0..7 = the source
+// state, 0x0c = nothing). cas a b: byte a -> byte b; read a: byte a -> byte a; read nil:
+// identity; an op naming a value the register never holds: nothing. A write (every state ->
+// byte b, an OR of the bytes, which no permutation does) is marked hi == OPS_FOLD with
+// lo = 8 * b. Each team keeps its live slots' ops in an LDS table read at a uniform address,
+// so the pull loop has one uniform branch (write or not) per op and no readlane.
+struct OpSel {
+  uint32_t lo, hi;
+};
+constexpr uint32_t OPS_FOLD = 0xffffffffu, SEL_NONE = 0x0c0c0c0cu;
+
+__device__ __forceinline__ OpSel sel_move(uint32_t s, uint32_t d) {  // byte s -> byte d
+  const uint32_t sh = (d & 3u) * 8u;
+  const uint32_t one = (SEL_NONE & ~(0xffu << sh)) | (s << sh);
+  return d < 4 ? OpSel{one, SEL_NONE} : OpSel{SEL_NONE, one};
+}
+
+__device__ __forceinline__ OpSel decode_op(uint32_t am, uint32_t bm) {
+  if (am == 0) return OpSel{SEL_NONE, SEL_NONE};  // names a value the register never holds
   if (bm) {
-    const uint32_t dst = ((uint32_t)__builtin_ctz(bm) * 8u) << 8;
-    if (am == 0xffu) return OPF_FOLD | dst;  // write: from any state
-    return (uint32_t)__builtin_ctz(am) * 8u | dst;
+    const uint32_t d = (uint32_t)__builtin_ctz(bm);
+    if (am == 0xffu) return OpSel{d * 8u, OPS_FOLD};  // write: from any state
+    return sel_move((uint32_t)__builtin_ctz(am), d);   // cas
   }
-  if (am == 0xffu) return OPF_IDENT;  // read nil: every state stays
-  const uint32_t a = (uint32_t)__builtin_ctz(am) * 8u;
-  return a | (a << 8);
+  if (am == 0xffu) return OpSel{0x03020100u, 0x07060504u};  // read nil: every state stays
+  const uint32_t a = (uint32_t)__builtin_ctz(am);
+  return sel_move(a, a);  // read a
+}
+
+// An op table is OP_TAB entries of LDS, 16-B aligned, used from entry OP_PAD on (slot k at
+// table[OP_PAD + k]): slot 3 + 4i lands on a 16-B boundary for the pull loop's pair reads.
+constexpr int OP_PAD = 1, OP_TAB = 36;
+
+// slots whose op is a write (lanes 0..31 of the calling wave read the team's table)
+__device__ __forceinline__ uint32_t fold_mask(const OpSel* ops) {
+  const int lane = threadIdx.x & 63;
+  return (uint32_t)__ballot(lane < 32 && ops[lane & 31].hi == OPS_FOLD);
 }
 
 // positions (of 8) whose mask lacks bit k (k < 3), one byte / replicated over 8 bytes
@@ -77,20 +101,26 @@ __device__ __forceinline__ uint64_t keep64(int k) {
   return k == 0 ? 0x5555555555555555ull : k == 1 ? 0x3333333333333333ull : 0x0f0f0f0f0f0f0f0full;
 }
 
-// op (wave-uniform) applied to word a (all 8 states), result bytes kept at positions
-// `keep` (8-bit, replicated as keep_all), then moved up by `up` positions. The flag tests
-// are scalar branches on a uniform value; the common MOVE path is shift, mask, shift.
-__device__ __forceinline__ uint64_t transfer(uint32_t op, uint64_t a, uint32_t keep, uint64_t keep_all, int up) {
-  if (op & (OPF_IDENT | OPF_NONE)) return (op & OPF_NONE) ? 0ull : (a & keep_all) << up;
-  uint32_t t;
-  if (op & OPF_FOLD) {
-    t = (uint32_t)a | (uint32_t)(a >> 32);
-    t |= t >> 16;
-    t |= t >> 8;
-  } else {
-    t = (uint32_t)(a >> (op & 63u));
-  }
-  return (uint64_t)(t & keep) << (((op >> 8) & 63u) + (uint32_t)up);
+__device__ __forceinline__ uint64_t perm64(OpSel s, uint64_t a) {
+  const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+  return ((uint64_t)__builtin_amdgcn_perm(hi, lo, s.hi) << 32) | __builtin_amdgcn_perm(hi, lo, s.lo);
+}
+__device__ __forceinline__ uint32_t fold8(uint64_t a) {  // OR of the 8 state bytes, in byte 0
+  uint32_t t = (uint32_t)a | (uint32_t)(a >> 32);
+  t |= t >> 16;
+  t |= t >> 8;
+  return t & 0xffu;
+}
+
+// op applied to word a (all 8 states) for a pull over a hi bit (positions unchanged)
+__device__ __forceinline__ uint64_t transfer(OpSel s, bool fold, uint64_t a) {
+  return fold ? (uint64_t)fold8(a) << s.lo : perm64(s, a);
+}
+// op applied for an in-word step over low bit k: result positions kept by `keep` (8-bit,
+// replicated as keep_all), then moved up by `up` positions
+__device__ __forceinline__ uint64_t transfer_lo(OpSel s, bool fold, uint64_t a, uint32_t keep, uint64_t keep_all,
+                                                int up) {
+  return fold ? (uint64_t)(fold8(a) & keep) << (s.lo + (uint32_t)up) : (perm64(s, a) & keep_all) << up;
 }
 
 // HBM tile mirrors: write-through sc1 stores, L1-bypassing sc1 loads
@@ -107,10 +137,11 @@ struct HbmTab {
 // One step's pulls and in-word closure for word w (LDS table B): R starts from R0 (pulls
 // from other tiles, computed by the caller), adds the pulls from the finalized words one
 // local hi bit below and the in-word closure. Returns popcount(R); *out = X | R.
-// opv: lane k holds slot k's decoded op (read with readlane, wave-uniform).
+// ops: the team's LDS op table (slot k); foldm: its write slots (wave-uniform).
 template <int HMAX, int BATCH>
 __device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero, uint32_t w, uint32_t live, int j,
-                                              int H, uint32_t opv, uint64_t R0, uint64_t* out) {
+                                              int H, const OpSel* ops, uint32_t foldm, uint64_t R0,
+                                              uint64_t* out) {
   const uint64_t X = B[w];
   uint64_t R = R0;
   const bool j_lo = j < 3;
@@ -120,16 +151,25 @@ __device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero
   // a batch are issued together (lanes without the bit read a zero word instead of taking a
   // branch), then the batch's ops are applied. Bits >= H read the zero word (w < 2^H).
   const uint32_t pm = has_j ? jh : w;  // bits this word pulls over
+  // the batch's four ops (slots b0+3 .. b0+6) come in two 16-B reads: slot 3 + 4i of an op
+  // table is 16-B aligned (OP_PAD)
+  static_assert(BATCH == 4, "op reads are two 16-B pairs");
   for (int b0 = 0; b0 < H; b0 += BATCH) {
+    const uint4* op4 = reinterpret_cast<const uint4*>(__builtin_assume_aligned(&ops[b0 + 3], 16));
+    const uint4 s01 = op4[0], s23 = op4[1];
     uint64_t v[BATCH];
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
       const uint32_t bit = 1u << (b0 + u);
       v[u] = *((pm & bit) ? &B[w ^ bit] : zero);
     }
+    // the selectors are needed here, after the data loads issued: keeps the compiler from
+    // sinking half of them into the branches below (one more LDS round trip per op)
+    asm volatile("" ::"v"(s01.x), "v"(s01.y), "v"(s01.z), "v"(s01.w), "v"(s23.x), "v"(s23.y), "v"(s23.z),
+                 "v"(s23.w));
+    const OpSel sel[4] = {{s01.x, s01.y}, {s01.z, s01.w}, {s23.x, s23.y}, {s23.z, s23.w}};
 #pragma unroll
-    for (int u = 0; u < BATCH; ++u)
-      R |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, b0 + u + 3), v[u], 0xffu, ~0ull, 0);
+    for (int u = 0; u < BATCH; ++u) R |= transfer(sel[u], (foldm >> (b0 + u + 3)) & 1u, v[u]);
   }
   if (!has_j) {
     const uint32_t notj = j_lo ? keep8(j) : 0xffu;
@@ -138,16 +178,16 @@ __device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero
     // ---- in-word closure: nlo passes over the live low ops other than j
     const uint32_t lo_ops = live & 7u & ~(j_lo ? (1u << j) : 0u);
     const int nlo = __popc(lo_ops);
+    const OpSel lo_sel[3] = {ops[0], ops[1], ops[2]};
     for (int pass = 0; pass < nlo; ++pass) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         if (lo_ops & (1u << k))
-          R |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, k), X | R, keep8(k) & notj,
-                        keep64(k) & notj64, 1 << k);
+          R |= transfer_lo(lo_sel[k], (foldm >> k) & 1u, X | R, keep8(k) & notj, keep64(k) & notj64, 1 << k);
       }
     }
     if (j_lo)  // the returning op, linearized last
-      R |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, j), X | R, notj, notj64, 1 << j);
+      R |= transfer_lo(ops[j], (foldm >> j) & 1u, X | R, notj, notj64, 1 << j);
   }
   if (R) B[w] = X | R;
   *out = X | R;
@@ -158,22 +198,32 @@ __device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero
 // tt = 0..nt-1; sync() ends every layer (the last one too: the return that follows reads
 // the last layer's words).
 template <int HMAX, int BATCH, class Sync>
-__device__ __forceinline__ unsigned long long run_layers(uint64_t* B, const uint64_t* zero, const uint32_t* words, const uint32_t* wofs,
-                                                        const uint32_t* binom, uint32_t live, int j,
-                                                        uint32_t opv, int tt, int nt, Sync&& sync) {
+__device__ __forceinline__ unsigned long long run_layers(uint64_t* B, const uint64_t* zero, const uint32_t* words,
+                                                        const uint32_t* wofs, const uint32_t* binom, uint32_t live,
+                                                        int j, const OpSel* ops, uint32_t foldm, int tt, int nt,
+                                                        Sync&& sync) {
   const int L = 32 - __clz((int)live);
   const int H = L > 3 ? L - 3 : 0;
   const uint32_t live_hi = live >> 3;
   unsigned long long expl = 0;
+  // words of popcount q below 2^H: a prefix of layer q of the sorted list. Each thread loads
+  // its next word index one word ahead (the next layer's first before the barrier), so the
+  // list load's latency hides behind a word's closure.
+  uint32_t nq = __builtin_amdgcn_readfirstlane(binom[H * BINOM_N]);
+  uint32_t o = __builtin_amdgcn_readfirstlane(wofs[0]);
+  uint32_t wn = (uint32_t)tt < nq ? words[o + tt] : 0u;
   for (int q = 0; q <= H; ++q) {
-    // words of popcount q below 2^H: a prefix of layer q of the sorted list
-    const uint32_t nq = __builtin_amdgcn_readfirstlane(binom[H * BINOM_N + q]);
-    const uint32_t o = __builtin_amdgcn_readfirstlane(wofs[q]);
     for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)nt) {
-      const uint32_t w = words[o + r];
+      const uint32_t w = wn;
+      if (r + nt < nq) wn = words[o + r + nt];
       if (w & ~live_hi) continue;
       uint64_t nv;
-      expl += close_word<HMAX, BATCH>(B, zero, w, live, j, H, opv, 0ull, &nv);
+      expl += close_word<HMAX, BATCH>(B, zero, w, live, j, H, ops, foldm, 0ull, &nv);
+    }
+    if (q < H) {
+      nq = __builtin_amdgcn_readfirstlane(binom[H * BINOM_N + q + 1]);
+      o = __builtin_amdgcn_readfirstlane(wofs[q + 1]);
+      wn = (uint32_t)tt < nq ? words[o + tt] : 0u;
     }
     sync();
   }
@@ -268,7 +318,7 @@ struct StreamWin {
 
 // decode the step header at pos; lanes < ninv of the calling wave store their op words
 __device__ __forceinline__ uint32_t read_step(const StreamWin& sw, int64_t pos, int lane, bool writer,
-                                             uint32_t* opt, int* ninv_out) {
+                                             OpSel* opt, int* ninv_out) {
   const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sw.at(pos));  // wave-uniform
   const int ninv = (int)(H0 >> 27);
   const uint32_t w = sw.at(pos + 1 + lane);
@@ -280,7 +330,7 @@ __device__ __forceinline__ uint32_t read_step(const StreamWin& sw, int64_t pos, 
 // Histories dequeued one at a time by a team of TEAM threads (a wave or a workgroup) that
 // keeps the whole table in LDS (B, 2^(TLOG-3) words).
 template <int TEAM, int TLOG>
-__device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, const uint64_t* zero, uint32_t* opt,
+__device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, const uint64_t* zero, OpSel* opt,
                                              int* sQ,
                                              unsigned long long* sExpl, const uint32_t* words,
                                              const uint32_t* wofs, const uint32_t* binom, int tt,
@@ -314,7 +364,7 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
       team_sync<TEAM>();
       const uint32_t live = H0 & 0x3fffffu;
       const int j = (int)((H0 >> 22) & 31u);
-      const uint32_t opv = opt[lane & 31];  // lane k: slot k's op, read with readlane
+      const uint32_t foldm = fold_mask(opt);
       const int Lw = 32 - __clz((int)live);
       const int nwt = 1 << (Lw > 3 ? Lw - 3 : 0);
       unsigned long long t0 = 0, nzx = 0, e0 = expl;
@@ -322,7 +372,8 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
         for (int i = tt; i < nwt; i += TEAM) nzx += B[i] != 0;
         t0 = __builtin_amdgcn_s_memrealtime();
       }
-      expl += run_layers<HMAX, 4>(B, zero, words, wofs, binom, live, j, opv, tt, TEAM, [] { team_sync<TEAM>(); });
+      expl += run_layers<HMAX, 4>(B, zero, words, wofs, binom, live, j, opt, foldm, tt, TEAM,
+                                  [] { team_sync<TEAM>(); });
       if (p.lhist) {
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
         unsigned long long nza = 0;
@@ -378,13 +429,16 @@ __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
   __shared__ uint32_t sWords[1 << HMAX];  // words sorted by (popcount, value)
   __shared__ uint32_t sWOff[HMAX + 2];
   __shared__ uint32_t sBinom[BINOM_N * BINOM_N];
-  __shared__ uint32_t sOp[NTEAM][32];
+  __shared__ __attribute__((aligned(16))) OpSel sOp[NTEAM][OP_TAB];
   __shared__ int sQ[NTEAM];
   __shared__ uint64_t sZero;  // the word pulls of absent bits read
   __shared__ unsigned long long sExpl[NTEAM];
   const int tid = threadIdx.x, team = tid / 64, tt = tid % 64;
   init_tables(sBinom, sWOff, HMAX, WAVE_WG);
   if (tid == 0) sZero = 0;
+  // every op-table entry moves nothing until its slot is invoked (v_perm selector bytes
+  // 13..15 would make 0xff out of a zero word)
+  for (int i = tid; i < NTEAM * OP_TAB; i += WAVE_WG) (&sOp[0][0])[i] = OpSel{SEL_NONE, SEL_NONE};
   for (int v = tid; v < (1 << HMAX); v += WAVE_WG) {  // colex rank within its popcount layer
     uint32_t rank = 0;
     int i = 0;
@@ -393,7 +447,7 @@ __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
   }
   __syncthreads();
   unsigned long long st_fout = 0, st_steps = 0;
-  history_loop<64, DENSE_WAVE_LMAX>(p, &sTab[team << HMAX], &sZero, sOp[team], &sQ[team], &sExpl[team], sWords, sWOff,
+  history_loop<64, DENSE_WAVE_LMAX>(p, &sTab[team << HMAX], &sZero, sOp[team] + OP_PAD, &sQ[team], &sExpl[team], sWords, sWOff,
                                     sBinom, tt, st_fout, st_steps);
   flush_stats(p, st_fout, st_steps, tt == 0);
 }
@@ -491,7 +545,8 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   __shared__ uint64_t sTab[1 << HSOLO];
   __shared__ uint32_t sWOff[DENSE_WORD_BITS + 2];
   __shared__ uint32_t sBinom[BINOM_N * BINOM_N];
-  __shared__ uint32_t sOp[32];
+  __shared__ __attribute__((aligned(16))) OpSel sOpT[OP_TAB];
+  OpSel* const sOp = sOpT + OP_PAD;
   __shared__ int sQ, sCmd, sAbort;
   __shared__ long long sPos;
   __shared__ unsigned sAny;
@@ -501,6 +556,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   init_tables(sBinom, sWOff, DENSE_WORD_BITS, 1024);
   if (tid == 0) sAbort = 0, sZero = 0;
+  if (tid < OP_TAB) sOpT[tid] = OpSel{SEL_NONE, SEL_NONE};  // (see dense_wave_kernel)
   __syncthreads();
   unsigned long long st_fout = 0, st_steps = 0;
 
@@ -536,7 +592,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.stream[hpos]);
     const uint32_t live = H0 & 0x3fffffu;
     const int j = (int)((H0 >> 22) & 31u);
-    const uint32_t opv = sOp[lane & 31];
+    const uint32_t foldm = fold_mask(sOp);
     const uint32_t live_loc = live & ((1u << DENSE_LMAX) - 1), live_team = live >> DENSE_LMAX;
     const bool active = ((uint32_t)rank & ~live_team) == 0;
     const int jt = j >= DENSE_LMAX ? j - DENSE_LMAX : -1;
@@ -558,9 +614,12 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
         wait_flags(p, flags, rank, preds, tok0 + q + 1, &sAbort);
         ph[0] += now() - tp;
         tp = now();
-        const uint32_t nq = sBinom[H * BINOM_N + q], o = sWOff[q];
+        const uint32_t nq = __builtin_amdgcn_readfirstlane(sBinom[H * BINOM_N + q]);
+        const uint32_t o = __builtin_amdgcn_readfirstlane(sWOff[q]);
+        uint32_t wn = (uint32_t)tid < nq ? p.words[o + tid] : 0u;
         for (uint32_t r = (uint32_t)tid; r < nq; r += 1024) {
-          const uint32_t w = p.words[o + r];
+          const uint32_t w = wn;
+          if (r + 1024 < nq) wn = p.words[o + r + 1024];
           if (w & ~live_hi) continue;
           // pulls from the tiles one team bit below: none for masks holding a local j
           // (configs holding j are never expanded); a tile holding j takes only T_j of r \ j
@@ -569,7 +628,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
             for (uint32_t m = preds; m; m &= m - 1) {
               const int b = __builtin_ctz(m);
               const uint64_t v = HbmTab::ld(mirror(rank ^ (1 << b)) + mo + r);
-              R0 |= transfer((uint32_t)__builtin_amdgcn_readlane((int)opv, DENSE_LMAX + b), v, 0xffu, ~0ull, 0);
+              R0 |= transfer(sOp[DENSE_LMAX + b], (foldm >> (DENSE_LMAX + b)) & 1u, v);
             }
           }
           uint64_t nv;
@@ -579,7 +638,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
             if (R0) sTab[w] = nv;
             expl += (uint32_t)__popcll(R0);
           } else {
-            expl += close_word<HSOLO, 4>(sTab, &sZero, w, live_loc, j, H, opv, R0, &nv);
+            expl += close_word<HSOLO, 4>(sTab, &sZero, w, live_loc, j, H, sOp, foldm, R0, &nv);
           }
           HbmTab::st(mine + mo + r, nv);  // mirrors are in word-list order
         }
@@ -646,8 +705,8 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
       const int j = (int)((H0 >> 22) & 31u);
       bool survived;
       if ((live >> DENSE_LMAX) == 0) {  // narrow step: the leader alone (other tiles empty)
-        const uint32_t opv = sOp[lane & 31];
-        expl += run_layers<HSOLO, 4>(sTab, &sZero, p.words, sWOff, sBinom, live, j, opv, tid, 1024,
+        const uint32_t foldm = fold_mask(sOp);
+        expl += run_layers<HSOLO, 4>(sTab, &sZero, p.words, sWOff, sBinom, live, j, sOp, foldm, tid, 1024,
                                      [] { __syncthreads(); });
         survived = __syncthreads_or(return_slot(sTab, live, j, tid, 1024, st_fout) != 0);
       } else {  // wide step: every tile
@@ -657,7 +716,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
           st_agent(&ctl->pos, hpos);
           st_agent(&ctl->any, 0u);
         }
-        if (tid < 32) st_agent(&ctl->ops[tid], sOp[tid]);
+        if (tid < 64) st_agent(&ctl->ops[tid], (&sOp[0].lo)[tid]);
         if (!bar()) break;
         survived = team_step(hpos);
         team_cycles += __builtin_amdgcn_s_memrealtime() - t0;
@@ -689,7 +748,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
         sCmd = ok ? ld_agent(&ctl->cmd) : CMD_EXIT;
         sPos = ld_agent(&ctl->pos);
       }
-      if (tid < 32) sOp[tid] = ld_agent(&ctl->ops[tid]);
+      if (tid < 64) (&sOp[0].lo)[tid] = ld_agent(&ctl->ops[tid]);
       __syncthreads();
       if (sCmd != CMD_STEP) break;
       team_step(sPos);
