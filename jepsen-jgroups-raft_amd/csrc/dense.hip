@@ -574,6 +574,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   const int h = p.team_hist[team];
   TeamCtl* const ctl = (TeamCtl*)p.ctl + team;
   unsigned long long* const flags = p.flags + base;
+  const int lb = p.team_lbits[team];  // local slots of every tile (<= DENSE_LMAX)
   auto mirror = [&](int r) { return p.mirror + ((size_t)(base + r) << HSOLO); };
   uint64_t* const mine = mirror(rank);
   auto bar = [&]() { return team_bar(ctl, G, p.abort, &sAbort); };
@@ -593,21 +594,21 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     const uint32_t live = H0 & 0x3fffffu;
     const int j = (int)((H0 >> 22) & 31u);
     const uint32_t foldm = fold_mask(sOp);
-    const uint32_t live_loc = live & ((1u << DENSE_LMAX) - 1), live_team = live >> DENSE_LMAX;
+    const uint32_t live_loc = live & ((1u << lb) - 1), live_team = live >> lb;
     const bool active = ((uint32_t)rank & ~live_team) == 0;
-    const int jt = j >= DENSE_LMAX ? j - DENSE_LMAX : -1;
+    const int jt = j >= lb ? j - lb : -1;
     const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
     const int Lloc = live_loc ? 32 - __clz((int)live_loc) : 0;
     const int H = Lloc > 3 ? Lloc - 3 : 0;
     const uint32_t live_hi = live_loc >> 3;
     // tiles this one pulls from: r \ b for its team bits (only r \ j when r holds j)
     const uint32_t preds = tile_j ? (1u << jt) : ((uint32_t)rank & live_team);
-    const bool jloc_hi = j >= 3 && j < DENSE_LMAX;
+    const bool jloc_hi = j >= 3 && j < lb;
     uint64_t anyv = 0;
     ph[5] += 1;
     if (active) {
       // mirror position of layer q's first word: words below 2^H in (popcount, value) order,
-      // so positions stay below 2^H <= 2^(DENSE_LMAX-3), the mirror's size
+      // so positions stay below 2^H <= 2^(lb-3) <= 2^(DENSE_LMAX-3), the mirror's size
       uint32_t mo = 0;
       for (int q = 0; q <= H; ++q) {
         unsigned long long tp = now();
@@ -616,31 +617,50 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
         tp = now();
         const uint32_t nq = __builtin_amdgcn_readfirstlane(sBinom[H * BINOM_N + q]);
         const uint32_t o = __builtin_amdgcn_readfirstlane(sWOff[q]);
-        uint32_t wn = (uint32_t)tid < nq ? p.words[o + tid] : 0u;
-        for (uint32_t r = (uint32_t)tid; r < nq; r += 1024) {
-          const uint32_t w = wn;
-          if (r + 1024 < nq) wn = p.words[o + r + 1024];
-          if (w & ~live_hi) continue;
-          // pulls from the tiles one team bit below: none for masks holding a local j
-          // (configs holding j are never expanded); a tile holding j takes only T_j of r \ j
-          uint64_t R0 = 0;
-          if (tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u))) {
-            for (uint32_t m = preds; m; m &= m - 1) {
-              const int b = __builtin_ctz(m);
-              const uint64_t v = HbmTab::ld(mirror(rank ^ (1 << b)) + mo + r);
-              R0 |= transfer(sOp[DENSE_LMAX + b], (foldm >> (DENSE_LMAX + b)) & 1u, v);
-            }
+        // this thread's words of the layer (at most TW: C(14, 7) = 3432 <= TW * 1024). Their
+        // cross-tile pulls go out together per predecessor tile: one HBM round trip per
+        // predecessor and layer, not one per word.
+        constexpr int TW = 4;
+        static_assert(TW * 1024 >= 3432, "a layer of a 17-bit tile fits TW words per thread");
+        uint32_t wl[TW];
+        uint64_t R0[TW];
+#pragma unroll
+        for (int k = 0; k < TW; ++k) {
+          const uint32_t r = (uint32_t)tid + (uint32_t)k * 1024u;
+          wl[k] = r < nq ? p.words[o + r] : ~0u;  // ~0u: no word (fails the live test)
+          R0[k] = 0;
+        }
+        for (uint32_t m = preds; m; m &= m - 1) {
+          const int b = __builtin_ctz(m);
+          const OpSel sb = sOp[lb + b];
+          const bool fb = (foldm >> (lb + b)) & 1u;
+          const uint64_t* src = mirror(rank ^ (1 << b)) + mo + tid;
+          uint64_t v[TW];
+#pragma unroll
+          for (int k = 0; k < TW; ++k) {
+            const uint32_t w = wl[k];
+            // pulls from the tiles one team bit below: none for masks holding a local j
+            // (configs holding j are never expanded); a tile holding j takes only T_j of r \ j
+            const bool pull = !(w & ~live_hi) && (tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u)));
+            v[k] = pull ? HbmTab::ld(src + k * 1024) : 0ull;
           }
+#pragma unroll
+          for (int k = 0; k < TW; ++k) R0[k] |= transfer(sb, fb, v[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < TW; ++k) {
+          const uint32_t w = wl[k];
+          if (w & ~live_hi) continue;
           uint64_t nv;
           if (tile_j) {  // every mask here holds j: linearized last, from tile r \ j
             const uint64_t X = sTab[w];
-            nv = X | R0;
-            if (R0) sTab[w] = nv;
-            expl += (uint32_t)__popcll(R0);
+            nv = X | R0[k];
+            if (R0[k]) sTab[w] = nv;
+            expl += (uint32_t)__popcll(R0[k]);
           } else {
-            expl += close_word<HSOLO, 4>(sTab, &sZero, w, live_loc, j, H, sOp, foldm, R0, &nv);
+            expl += close_word<HSOLO, 4>(sTab, &sZero, w, live_loc, j, H, sOp, foldm, R0[k], &nv);
           }
-          HbmTab::st(mine + mo + r, nv);  // mirrors are in word-list order
+          HbmTab::st(mine + mo + tid + k * 1024, nv);  // mirrors are in word-list order
         }
         mo += nq;
         __syncthreads();
@@ -704,7 +724,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
       const uint32_t live = H0 & 0x3fffffu;
       const int j = (int)((H0 >> 22) & 31u);
       bool survived;
-      if ((live >> DENSE_LMAX) == 0) {  // narrow step: the leader alone (other tiles empty)
+      if ((live >> lb) == 0) {  // narrow step: the leader alone (other tiles empty)
         const uint32_t foldm = fold_mask(sOp);
         expl += run_layers<HSOLO, 4>(sTab, &sZero, p.words, sWOff, sBinom, live, j, sOp, foldm, tid, 1024,
                                      [] { __syncthreads(); });

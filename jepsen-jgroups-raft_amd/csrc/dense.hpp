@@ -46,7 +46,8 @@ struct DenseParams {
   int32_t n_team_wgs;
   const int32_t* wg_team;       // [n_team_wgs] team of each workgroup
   const int32_t* team_base;     // [teams] first workgroup
-  const int8_t* team_bits;      // [teams] t: 2^t workgroups, history width <= 17 + t
+  const int8_t* team_bits;      // [teams] t: 2^t workgroups, history width <= lb + t
+  const int8_t* team_lbits;     // [teams] lb: local slots per tile (<= DENSE_LMAX)
   const int32_t* team_hist;     // [teams] history id
   uint64_t* mirror;             // [n_team_wgs][2^(DENSE_LMAX-3)] published tile words
   unsigned long long* flags;    // [n_team_wgs] layer tokens (zeroed before launch)

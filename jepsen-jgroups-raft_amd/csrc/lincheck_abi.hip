@@ -128,13 +128,14 @@ struct lc_plan {
   // dense closure tables (narrow cas-register histories; dense.hpp)
   std::vector<int> dense_b, dense_w, dense_x;  // block / wave / wide teams, heaviest first
   DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dwords, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
-  DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_thist;
+  DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_tlbits, d_thist;
   struct StepBytes { double lds, hbm; };
   std::vector<StepBytes> dalg;     // per dense step: algorithmic bytes
   std::vector<int64_t> dalg_off;    // [n_hist + 1] first step of each history in dalg
   int64_t dstream_words = 0;
   int dgrid_b = 0, dgrid_w = 0;
   int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
+  int tile_lbits = DENSE_LMAX;                        // LC_TILE_LBITS: local slots per tile
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_w0 = nullptr, ev_w1 = nullptr;  // per dense kernel
@@ -225,6 +226,7 @@ struct lc_plan {
     // dense-path knobs (tests): workgroups tile teams may take per launch, widest history
     if ((e = getenv("LC_TILE_WGS")) && atoi(e) > 0) tile_cap = atoi(e);
     if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
+    if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
     // test hooks: shrink the keys kernel's per-workgroup capacities to force the fallback
     if ((e = getenv("LC_KCAP")) && atoll(e) > 0) kfcap = klcap = atoll(e);
     // test hooks: tiny cells / overflow buckets exercise the overflow and regrow paths
@@ -399,8 +401,16 @@ struct lc_plan {
     const int cap = std::max(1, std::min(tile_cap, dgrid_b));
     std::vector<std::vector<int>> launches(1);
     int used = 0;
+    // local slots per tile: tile_lbits (<= DENSE_LMAX, the LDS tile), raised where the team
+    // would not fit the chip's workgroups; a team larger than `cap` gets a launch of its own
+    int grid_log = 0;
+    while ((2 << grid_log) <= dgrid_b) ++grid_log;
+    auto lbits_of = [&](int h) {
+      const int lw = enc.live_max[h];
+      return std::min(DENSE_LMAX, std::max(lw - grid_log, std::min(tile_lbits, lw - 1)));
+    };
     for (int h : dense_x) {
-      const int g = 1 << (enc.live_max[h] - DENSE_LMAX);
+      const int g = 1 << (enc.live_max[h] - lbits_of(h));
       if (used + g > cap && !launches.back().empty()) {
         launches.emplace_back();
         used = 0;
@@ -410,13 +420,20 @@ struct lc_plan {
     }
     size_t max_wgs = 0, max_teams = 0;
     std::vector<std::vector<int32_t>> l_wgteam(launches.size()), l_base(launches.size()), l_hist(launches.size());
-    std::vector<std::vector<int8_t>> l_bits(launches.size());
+    std::vector<std::vector<int8_t>> l_bits(launches.size()), l_lbits(launches.size());
     for (size_t l = 0; l < launches.size(); ++l) {
       int b = 0;
       for (int h : launches[l]) {
-        const int t = enc.live_max[h] - DENSE_LMAX;
+        const int t = enc.live_max[h] - lbits_of(h);
+        // the kernel trusts these: a tile is at most the 17-bit LDS table and a team's
+        // workgroups must all be resident at once
+        if (lbits_of(h) > DENSE_LMAX || lbits_of(h) < 4 || t < 1 || (1 << t) > dgrid_b) {
+          last_error = "dense tile team shape out of range";
+          return LC_E_INTERNAL;
+        }
         l_base[l].push_back(b);
         l_bits[l].push_back((int8_t)t);
+        l_lbits[l].push_back((int8_t)lbits_of(h));
         l_hist[l].push_back(h);
         for (int r = 0; r < (1 << t); ++r) l_wgteam[l].push_back((int32_t)l_base[l].size() - 1);
         b += 1 << t;
@@ -432,6 +449,7 @@ struct lc_plan {
       HIP_TRY(d_wgteam.ensure(max_wgs * 4));
       HIP_TRY(d_tbase.ensure(max_teams * 4));
       HIP_TRY(d_tbits.ensure(max_teams));
+      HIP_TRY(d_tlbits.ensure(max_teams));
       HIP_TRY(d_thist.ensure(max_teams * 4));
       HIP_TRY(hipMemsetAsync(d_abort.p, 0, 16, stream));
     }
@@ -460,12 +478,14 @@ struct lc_plan {
         HIP_TRY(hipMemcpyAsync(d_wgteam.p, l_wgteam[l].data(), twgs * 4, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(d_tbase.p, l_base[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(d_tbits.p, l_bits[l].data(), nt, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(d_tlbits.p, l_lbits[l].data(), nt, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(d_thist.p, l_hist[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemsetAsync(d_tflags.p, 0, (size_t)twgs * 8, stream));
         HIP_TRY(hipMemsetAsync(d_ctl.p, 0, (size_t)nt * dense_ctl_bytes(), stream));
         q.wg_team = d_wgteam.as<int32_t>();
         q.team_base = d_tbase.as<int32_t>();
         q.team_bits = d_tbits.as<int8_t>();
+        q.team_lbits = d_tlbits.as<int8_t>();
         q.team_hist = d_thist.as<int32_t>();
         q.mirror = d_mirror.as<uint64_t>();
         q.flags = d_tflags.as<unsigned long long>();
