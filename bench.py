@@ -45,7 +45,7 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int):
         t0 = time.perf_counter()
         oracle.check_many(model, h.select(probe), n_threads=threads)
         dt = max(time.perf_counter() - t0, 1e-3)  # one key per thread ~ per-key latency
-        keys = max(threads, min(n, int(budget_s / dt * threads)))
+        keys = min(n, max(threads, int(budget_s / dt * threads)))
         sample = list(range(keys))
         hs = h.select(sample)
         t0 = time.perf_counter()
@@ -55,17 +55,18 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int):
         used = threads
     else:
         # one history: the oracle is single-threaded like Knossos's per-history search;
-        # time a prefix of the history that fits the budget
-        frac = 1.0
+        # time the longest prefix that fits the budget, growing from a short one (a wide
+        # history's search cost grows much faster than its length)
+        m = min(h.n, 2000)
         while True:
-            m = int(h.n * frac)
-            hs = synth.truncate(h, m) if frac < 1.0 else h
+            hs = synth.truncate(h, m) if m < h.n else h
             t0 = time.perf_counter()
             res = oracle.check_many(model, hs, n_threads=1, max_configs=0)
             wall = time.perf_counter() - t0
-            if wall <= budget_s * 1.5 or frac < 0.01:
+            log(f"[cpu baseline] prefix of {m} entries: {wall:.2f}s")
+            if m >= h.n or wall >= budget_s / 4:
                 break
-            frac *= max(0.05, budget_s / wall * 0.8)
+            m = min(h.n, int(m * min(4.0, max(1.5, budget_s / 4 / max(wall, 1e-3)))))
         sample = [0]
         desc = f"first {hs.n} of {h.n} entries of the single history, 1 thread"
         used = 1
