@@ -134,23 +134,17 @@ struct HbmTab {
 };
 
 
-// One step's pulls and in-word closure for word w (LDS table B): R starts from R0 (pulls
-// from other tiles, computed by the caller), adds the pulls from the finalized words one
-// local hi bit below and the in-word closure. Returns popcount(R); *out = X | R.
+// Pulls of word w over its hi bits from the finalized words one hi bit below (LDS table B):
+// the bulk of a word's closure, needing nothing from other tiles. BATCH bits at a time: the
+// loads of a batch are issued together (lanes without the bit read a zero word instead of
+// taking a branch), then the batch's ops are applied. Bits >= H read the zero word (w < 2^H).
 // ops: the team's LDS op table (slot k); foldm: its write slots (wave-uniform).
-template <int HMAX, int BATCH>
-__device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero, uint32_t w, uint32_t live, int j,
-                                              int H, const OpSel* ops, uint32_t foldm, uint64_t R0,
-                                              uint64_t* out) {
-  const uint64_t X = B[w];
-  uint64_t R = R0;
-  const bool j_lo = j < 3;
-  const uint32_t jh = j_lo ? 0u : 1u << (j - 3);
-  const bool has_j = (w & jh) != 0;
-  // ---- pulls from the finalized words one hi bit below, BATCH bits at a time: the loads of
-  // a batch are issued together (lanes without the bit read a zero word instead of taking a
-  // branch), then the batch's ops are applied. Bits >= H read the zero word (w < 2^H).
-  const uint32_t pm = has_j ? jh : w;  // bits this word pulls over
+template <int BATCH>
+__device__ __forceinline__ uint64_t pull_hi(const uint64_t* B, const uint64_t* zero, uint32_t w, int j, int H,
+                                           const OpSel* ops, uint32_t foldm) {
+  const uint32_t jh = j < 3 ? 0u : 1u << (j - 3);
+  const uint32_t pm = (w & jh) ? jh : w;  // bits this word pulls over (only j when it holds j)
+  uint64_t R = 0;
   // the batch's four ops (slots b0+3 .. b0+6) come in two 16-B reads: slot 3 + 4i of an op
   // table is 16-B aligned (OP_PAD)
   static_assert(BATCH == 4, "op reads are two 16-B pairs");
@@ -171,7 +165,17 @@ __device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) R |= transfer(sel[u], (foldm >> (b0 + u + 3)) & 1u, v[u]);
   }
-  if (!has_j) {
+  return R;
+}
+
+// The rest of word w's closure, given R = its pulls (hi bits and other tiles): the in-word
+// closure over the 3 low bits, then the store. Returns popcount(R); *out = X | R.
+__device__ __forceinline__ uint32_t finish_word(uint64_t* B, uint32_t w, uint32_t live, int j, const OpSel* ops,
+                                               uint32_t foldm, uint64_t R, uint64_t* out) {
+  const uint64_t X = B[w];
+  const bool j_lo = j < 3;
+  const uint32_t jh = j_lo ? 0u : 1u << (j - 3);
+  if (!(w & jh)) {
     const uint32_t notj = j_lo ? keep8(j) : 0xffu;
     const uint64_t notj64 = j_lo ? keep64(j) : ~0ull;
     R &= notj64;  // configs holding j come only from T_j
@@ -192,6 +196,15 @@ __device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero
   if (R) B[w] = X | R;
   *out = X | R;
   return (uint32_t)__popcll(R);
+}
+
+// One step's closure of word w: R0 (pulls from other tiles, computed by the caller) plus the
+// hi-bit pulls and the in-word closure.
+template <int HMAX, int BATCH>
+__device__ __forceinline__ uint32_t close_word(uint64_t* B, const uint64_t* zero, uint32_t w, uint32_t live, int j,
+                                              int H, const OpSel* ops, uint32_t foldm, uint64_t R0,
+                                              uint64_t* out) {
+  return finish_word(B, w, live, j, ops, foldm, R0 | pull_hi<BATCH>(B, zero, w, j, H, ops, foldm), out);
 }
 
 // The closure layers of one step on an LDS table, words split over the team's threads
@@ -612,9 +625,6 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
       uint32_t mo = 0;
       for (int q = 0; q <= H; ++q) {
         unsigned long long tp = now();
-        wait_flags(p, flags, rank, preds, tok0 + q + 1, &sAbort);
-        ph[0] += now() - tp;
-        tp = now();
         const uint32_t nq = __builtin_amdgcn_readfirstlane(sBinom[H * BINOM_N + q]);
         const uint32_t o = __builtin_amdgcn_readfirstlane(sWOff[q]);
         // this thread's words of the layer (at most TW: C(14, 7) = 3432 <= TW * 1024). Their
@@ -629,6 +639,17 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
           const uint32_t r = (uint32_t)tid + (uint32_t)k * 1024u;
           wl[k] = r < nq ? p.words[o + r] : ~0u;  // ~0u: no word (fails the live test)
           R0[k] = 0;
+        }
+        // the hi-bit pulls read only this tile's finished layers: done before waiting for the
+        // predecessors' layer q (a tile holding j pulls nothing locally)
+#pragma unroll
+        for (int k = 0; k < TW; ++k)
+          if (!tile_j && !(wl[k] & ~live_hi)) R0[k] = pull_hi<4>(sTab, &sZero, wl[k], j, H, sOp, foldm);
+        {
+          const unsigned long long tw = now();
+          wait_flags(p, flags, rank, preds, tok0 + q + 1, &sAbort);
+          ph[0] += now() - tw;
+          tp += now() - tw;  // (compute excludes the wait)
         }
         for (uint32_t m = preds; m; m &= m - 1) {
           const int b = __builtin_ctz(m);
@@ -658,7 +679,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
             if (R0[k]) sTab[w] = nv;
             expl += (uint32_t)__popcll(R0[k]);
           } else {
-            expl += close_word<HSOLO, 4>(sTab, &sZero, w, live_loc, j, H, sOp, foldm, R0[k], &nv);
+            expl += finish_word(sTab, w, live_loc, j, sOp, foldm, R0[k], &nv);
           }
           HbmTab::st(mine + mo + tid + k * 1024, nv);  // mirrors are in word-list order
         }
