@@ -177,6 +177,64 @@ def bench_c5(args, rank, world, dist, barrier_sync):
     return out
 
 
+def bench_partition(args, rank, world, dist, barrier_sync):
+    """Axis 2: ONE cas-register history (c2 or c4) searched by all ranks at once,
+    its frontier partitioned by config hash, one all-to-all of candidates per BFS level (RCCL
+    over xGMI). Strong scaling: every rank works on the same history."""
+    from lincheck import partition
+    tdist = dist[1] if dist else None
+    h = synth.gen_config(args.workload, scale=args.scale)
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    runs = []
+    for i in range(args.warmup + args.steps):
+        if i == args.warmup:
+            barrier_sync()
+            t0 = time.perf_counter()
+        r = partition.check_partitioned(h, tdist=tdist, device_index=local)
+        if i >= args.warmup:
+            runs.append(r)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        torch, td = dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        td.all_reduce(t, op=td.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        return None
+    r = runs[-1]
+    k_s = sum(x["kernel_ms"] for x in runs) / len(runs) / 1e3
+    achieved = r["alg_bytes"] / k_s / 1e9 if k_s > 0 else 0.0
+    return {
+        "metric": "history ops verified/sec (+ configs explored/sec, % HBM roofline)",
+        "value": h.n_ops() * args.steps / elapsed,
+        "unit": "history ops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (simulated linearizable SUT, SURVEY §8(d) seeds)",
+        "config": {"workload": f"{args.workload}: one register history, frontier partitioned "
+                               f"by config hash over {world} rank(s)",
+                   "ops": h.n_ops(), "scale": args.scale,
+                   "parallelism": f"axis 2: {world} GPU(s), one all-to-all per BFS level"},
+        "configs_explored_per_s": r["explored"] * args.steps / elapsed,
+        "verdict": {"valid": r["valid"], "explored": r["explored"], "steps": r["steps"],
+                    "levels": r["levels"], "exchanged_bytes": r["exchanged_bytes"]},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "lc::part_expand + lc::part_absorb (rank 0)",
+                     "kernel_ms": k_s * 1e3, "alg_bytes_per_launch": r["alg_bytes"],
+                     "note": "per check (all levels); the wall time is dominated by the per-level "
+                             "host round trip (count exchange + all-to-all), see DESIGN.md §6"},
+        "cpu_baseline": None,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,6 +244,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--partition", action="store_true",
+                    help="axis 2: one history (c2/c4) with its frontier partitioned over ranks")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC passes (or absent)")
     args = ap.parse_args()
@@ -207,8 +267,10 @@ def main():
             dist[1].barrier()
             dist[0].cuda.synchronize()
 
-    if args.workload == "c5":
-        out = bench_c5(args, rank, world, dist, barrier_sync)
+    if args.workload == "c5" or args.partition:
+        if args.partition and args.workload not in ("c2", "c4"):
+            raise SystemExit("--partition runs one history: --workload c2 or c4")
+        out = (bench_partition if args.partition else bench_c5)(args, rank, world, dist, barrier_sync)
         if out is not None:
             print(json.dumps(out), flush=True)
         if dist:

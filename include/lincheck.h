@@ -159,6 +159,48 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
 void lc_plan_destroy(lc_plan* p);
 
+/* ---- one history, frontier partitioned over ranks (SURVEY §8(e) axis 2) ----
+ * A single huge cas-register history searched by `world` ranks (one process per GPU), each
+ * owning the configs whose hash maps to it. Replaces the same knossos.linear/analysis call as
+ * lc_check (register.clj:109-111) for ONE history, split across GPUs. The library runs each
+ * rank's kernels; the caller runs the collectives (lincheck/partition.py: torch.distributed,
+ * RCCL over xGMI). Per RETURN step t = 0, 1, ...:
+ *   lc_part_step_begin(t)
+ *   loop: lc_part_expand -> send_counts[world]; all-gather the counts (stop when every rank's
+ *         are all zero); lc_part_pack into the all-to-all input (contiguous by destination);
+ *         all-to-all; lc_part_absorb(received)
+ *   lc_part_step_end -> this rank's frontier size; all-reduce SUM: 0 => not linearizable at
+ *         step t (lc_part_results gives the :index triple and this rank's explored count;
+ *         the explored total is the SUM over ranks).
+ * `stream` is a hipStream_t (NULL = the default stream); buffers passed in are device memory
+ * of `device`. world <= 16; capacity_log2 (<= 26, 0 = 22) sizes each rank's lists (2^c
+ * configs) and hash sets (2^(c+1) words). Exceeding it returns LC_H_CAPACITY (-7).
+ * A plan is used by one thread at a time. */
+typedef struct lc_part lc_part;
+int32_t lc_part_create(int32_t device, int32_t model_kind, int64_t init_value, int64_t n,
+                       const int64_t* index, const int32_t* process, const int8_t* type,
+                       const int8_t* f, const int64_t* v0, const int64_t* v1, const int8_t* vflags,
+                       int32_t rank, int32_t world, int32_t capacity_log2, lc_part** out, char* err,
+                       int32_t err_len);
+/* info[0] RETURN steps, [1] history error (LC_H_*), [2] mask bits, [3] state bits,
+ * [4] invocations, [5] list capacity, [6] kernel ns so far (HIP events), [7] algorithmic
+ * HBM bytes so far */
+int32_t lc_part_info(lc_part* p, int64_t* info, int32_t n);
+int32_t lc_part_step_begin(lc_part* p, int64_t t, void* stream, char* err, int32_t err_len);
+int32_t lc_part_expand(lc_part* p, void* stream, int64_t* send_counts /*[world]*/, char* err,
+                       int32_t err_len);
+int32_t lc_part_pack(lc_part* p, void* stream, void* dst, int64_t dst_cap, char* err,
+                     int32_t err_len);
+/* recv = NULL absorbs this rank's own staged candidates (world 1 only) */
+int32_t lc_part_absorb(lc_part* p, void* stream, const void* recv, int64_t n, char* err,
+                       int32_t err_len);
+int32_t lc_part_step_end(lc_part* p, void* stream, int64_t* out_count, char* err, int32_t err_len);
+/* out4[0] this rank's explored count, [1] :index of step t's :ok completion, [2] of its
+ * invocation, [3] of step t-1's completion (-1 at t = 0) */
+int32_t lc_part_results(lc_part* p, int64_t t, void* stream, int64_t* out4, char* err,
+                        int32_t err_len);
+void lc_part_destroy(lc_part* p);
+
 #ifdef __cplusplus
 }
 #endif

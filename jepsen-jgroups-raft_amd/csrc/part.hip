@@ -1,0 +1,543 @@
+// part.hip — one cas-register history searched by several ranks at once, its frontier
+// partitioned by config hash (SURVEY §8(e) axis 2; knossos.linear/analysis [ext], §8(a) a5,
+// model register.clj:110). The library runs the per-rank work; the caller (lincheck/
+// partition.py, or any host with a collective library) moves candidates between ranks with
+// one all-to-all per BFS level (RCCL over xGMI under torch.distributed "nccl").
+//
+// Per RETURN step of slot j (bitj = 1 << j), every rank r holds F_r, its part of the frontier
+// (globally duplicate-free), and owns the configs c with owner(c & ~bitj) = r:
+//   level 0 : expand F_r: a config holding j goes DIRECT to the owner of c & ~bitj (its
+//             post-return image); every other config steps each pending op k not in its mask
+//             (cas-register: consistent iff the op's expected state is any/equal) -> c2.
+//   exchange: candidates travel to their owners (one all-to-all, counts gathered first).
+//   absorb  : DIRECT -> OUT set. Else insert c2 into the closure set S; a new c2 counts as
+//             explored and either holds j (linearized the returning op: its image c2 & ~bitj
+//             goes to OUT, same owner by construction) or joins the next level's list.
+//   level l : expand the new list (its configs never hold j), exchange, absorb ... until no
+//             rank produced a candidate. Then F_r = OUT_r; sum over ranks of |F_r| = 0 =>
+//             not linearizable at this RETURN.
+// S and OUT are open-addressing hash sets in HBM (atomicCAS on 64-bit words, linear probing)
+// whose words carry a 16-bit step epoch above the 48-bit key, so a new step needs no clear.
+// Survivors are compacted with one wave ballot + one global atomic per wave and list.
+// The explored count is a set cardinality per step, so it is independent of the rank count
+// and of arrival order: bit-exact with the single-GPU paths and the oracle.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/lincheck.h"
+#include "device_common.hpp"
+#include "encode.hpp"
+
+namespace lc {
+namespace {
+
+constexpr int PW_MAX = 16;                   // ranks
+constexpr int PS_MAX = 48;                   // slots (mask bits)
+constexpr int KEY_BITS = 48;                 // [state | mask] below the epoch
+constexpr uint64_t DIRECT = 1ull << 63;      // in transit: already returned, goes to OUT
+constexpr int PT = 256;                      // threads per workgroup
+constexpr uint32_t EPOCH_MAX = 0xffffu;
+
+enum : int { PF_OVERFLOW = 1 };
+
+// device counters of one rank (one D2H read per level)
+struct PartCtl {
+  unsigned long long cnt[PW_MAX];  // candidates per destination (this level)
+  unsigned long long lc[2];        // level lists (count)
+  unsigned long long fcount;       // frontier F
+  unsigned long long ocount;       // OUT list
+  unsigned long long scount;       // S inserts this step
+  unsigned long long explored;     // all steps
+  unsigned long long flags;
+  unsigned long long pad[5];
+};
+
+struct StepArgs {
+  uint64_t ops[PS_MAX];  // per slot: (uint32 b << 32) | uint32 a; a: expected state id (-1 any,
+                         // -2 never), b: new state id (-1 keep)
+  uint64_t live, bitj;
+  int32_t mask_bits, world, rank, pad;
+};
+
+__device__ __forceinline__ uint32_t owner_of(uint64_t k, uint32_t world) {
+  return (uint32_t)(((mix64(k) >> 32) * (uint64_t)world) >> 32);
+}
+
+// global-counter append: lanes with `pred` get distinct positions, one atomic per wave
+__device__ __forceinline__ unsigned long long wave_append_g(unsigned long long* counter, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if (m == 0) return 0;
+  const int lane = __lane_id();
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(m));
+  base = __shfl(base, leader, 64);
+  const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
+  return base + (unsigned long long)__popcll(below);
+}
+
+// insert key (< 2^48) into an epoch-tagged open-addressing set; 1 = new, 0 = present
+__device__ __forceinline__ int set_insert(uint64_t* T, uint64_t tmask, uint64_t key, uint64_t ep,
+                                          unsigned long long* flags) {
+  const uint64_t v = (ep << KEY_BITS) | key;
+  uint64_t i = mix64(key) & tmask;
+  for (uint64_t probe = 0; probe <= tmask; ++probe) {
+    uint64_t cur = ld_agent(&T[i]);
+    if (cur == v) return 0;
+    if ((cur >> KEY_BITS) != ep) {  // free in this epoch: claim it
+      const uint64_t old = atomicCAS((unsigned long long*)&T[i], (unsigned long long)cur, (unsigned long long)v);
+      if (old == cur) return 1;
+      if (old == v) return 0;
+      if ((old >> KEY_BITS) != ep) {  // raced with a stale word's owner? (cannot happen) retry
+        --probe;
+        continue;
+      }
+    }
+    i = (i + 1) & tmask;
+  }
+  atomicOr(flags, (unsigned long long)PF_OVERFLOW);
+  return 0;
+}
+
+// Expand: thread per (config, slot) pair of the list; candidates staged per destination
+// ([world][seg_cap]); counts may exceed seg_cap (the host then grows the staging and re-runs).
+__global__ void __launch_bounds__(PT) part_expand(StepArgs a, const uint64_t* __restrict__ list,
+                                                  const unsigned long long* __restrict__ count, uint32_t wd,
+                                                  uint64_t* __restrict__ stage, uint64_t seg_cap, PartCtl* ctl) {
+  const uint32_t n = (uint32_t)count[0] * wd;  // < 2^32: list_cap <= 2^26, wd <= 48
+  const uint64_t mmask = (1ull << a.mask_bits) - 1;
+  const uint32_t stride = gridDim.x * PT;
+  for (uint32_t it = blockIdx.x * PT; it < n; it += stride) {  // block-uniform trip count
+    const uint32_t i = it + threadIdx.x;
+    bool has = false;
+    uint64_t out = 0, route = 0;
+    if (i < n) {
+      const uint32_t ci = i / wd;
+      const uint64_t c = list[ci];
+      const int k = (int)(i - ci * wd);
+      if (c & a.bitj) {  // already linearized the returning op: its image goes straight to OUT
+        if (k == 0) {
+          route = c & ~a.bitj;
+          out = route | DIRECT;
+          has = true;
+        }
+      } else if (((a.live >> k) & 1) && !((c >> k) & 1)) {
+        const uint64_t op = a.ops[k];
+        const int32_t ea = (int32_t)(uint32_t)op, nb = (int32_t)(uint32_t)(op >> 32);
+        const int64_t st = (int64_t)(c >> a.mask_bits);
+        if (ea == -1 || ea == st) {
+          const uint64_t ns = nb < 0 ? (uint64_t)st : (uint64_t)nb;
+          out = (ns << a.mask_bits) | (c & mmask) | (1ull << k);
+          route = out & ~a.bitj;
+          has = true;
+        }
+      }
+    }
+    const uint32_t dst = has ? owner_of(route, (uint32_t)a.world) : 0u;
+    for (int d = 0; d < a.world; ++d) {
+      const unsigned long long pos = wave_append_g(&ctl->cnt[d], has && dst == (uint32_t)d);
+      if (has && dst == (uint32_t)d && pos < seg_cap) stage[(uint64_t)d * seg_cap + pos] = out;
+    }
+  }
+}
+
+// Absorb the candidates this rank owns: dedup into S / OUT, compact the survivors.
+__global__ void __launch_bounds__(PT) part_absorb(const uint64_t* __restrict__ recv, uint64_t n, uint64_t bitj,
+                                                  uint64_t* S, uint64_t smask, uint64_t* O, uint64_t omask,
+                                                  uint64_t ep, uint64_t* __restrict__ next,
+                                                  unsigned long long* next_count, uint64_t* __restrict__ outl,
+                                                  uint64_t list_cap, PartCtl* ctl) {
+  const uint64_t stride = (uint64_t)gridDim.x * PT;
+  unsigned long long expl = 0;
+  for (uint64_t it = (uint64_t)blockIdx.x * PT; it < n; it += stride) {
+    const uint64_t i = it + threadIdx.x;
+    bool news = false, newo = false, nl = false;
+    uint64_t key = 0, okey = 0;
+    if (i < n) {
+      key = recv[i];
+      if (key & DIRECT) {
+        okey = key & ~DIRECT;
+        newo = set_insert(O, omask, okey, ep, &ctl->flags);
+      } else {
+        news = set_insert(S, smask, key, ep, &ctl->flags);
+        if (news) {
+          if (key & bitj) {
+            okey = key & ~bitj;
+            newo = set_insert(O, omask, okey, ep, &ctl->flags);
+          } else {
+            nl = true;
+          }
+        }
+      }
+    }
+    expl += news;
+    const unsigned long long pn = wave_append_g(next_count, nl);
+    if (nl) {
+      if (pn < list_cap) next[pn] = key;
+      else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+    }
+    const unsigned long long po = wave_append_g(&ctl->ocount, newo);
+    if (newo) {
+      if (po < list_cap) outl[po] = okey;
+      else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
+  if (__lane_id() == 0 && expl) {
+    atomicAdd(&ctl->explored, expl);
+    atomicAdd(&ctl->scount, expl);
+  }
+}
+
+void set_msg(char* err, int32_t len, const char* fmt, ...) {
+  if (!err || len <= 0) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(err, (size_t)len, fmt, ap);
+  va_end(ap);
+}
+
+int bits_of(int64_t n) {
+  int b = 0;
+  while ((1ll << b) < n) ++b;
+  return b;
+}
+
+}  // namespace
+}  // namespace lc
+
+using namespace lc;
+
+struct lc_part {
+  int device = 0, rank = 0, world = 1;
+  Encoded enc;
+  int mask_bits = 0, state_bits = 0;
+  int slog = 0;               // S / OUT tables: 2^slog words
+  uint64_t list_cap = 0;      // level lists, F, OUT: entries
+  uint64_t seg_cap = 0;       // staging per destination
+  uint64_t* S = nullptr;
+  uint64_t* O = nullptr;
+  uint64_t* F = nullptr;      // frontier (this rank's part)
+  uint64_t* OUTL = nullptr;   // OUT list (next F)
+  uint64_t* Lb[2] = {nullptr, nullptr};
+  uint64_t* stage = nullptr;
+  PartCtl* ctl = nullptr;
+  PartCtl* hctl = nullptr;    // pinned host copy
+  int grid = 1024;
+  // measurement: HIP events around each kernel (on the caller's stream), algorithmic bytes
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool absorb_pending = false;
+  double kernel_ms = 0, alg_bytes = 0;
+  uint64_t listed = 0;  // entries of the list the last expand read
+  // step state
+  int64_t t = -1;
+  uint32_t epoch = 0;
+  StepArgs args{};
+  int level = 0, cur = 0;     // level lists: read list Lb[cur] at levels >= 1
+  uint32_t wd = 0;
+  uint64_t live = 0;
+  std::string last_error;
+
+  ~lc_part() {
+    for (void* q : {(void*)S, (void*)O, (void*)F, (void*)OUTL, (void*)Lb[0], (void*)Lb[1], (void*)stage,
+                    (void*)ctl})
+      if (q) (void)hipFree(q);
+    if (hctl) (void)hipHostFree(hctl);
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
+namespace {
+
+#define PT_TRY(expr)                                                          \
+  do {                                                                        \
+    hipError_t e_ = (expr);                                                   \
+    if (e_ != hipSuccess) {                                                   \
+      set_msg(err, err_len, "%s: %s", #expr, hipGetErrorString(e_));          \
+      return e_ == hipErrorOutOfMemory ? LC_E_MEMORY : LC_E_DEVICE;           \
+    }                                                                         \
+  } while (0)
+
+int part_read_ctl(lc_part* p, hipStream_t s, char* err, int32_t err_len) {
+  PT_TRY(hipMemcpyAsync(p->hctl, p->ctl, sizeof(PartCtl), hipMemcpyDeviceToHost, s));
+  PT_TRY(hipStreamSynchronize(s));
+  if (p->absorb_pending) {  // the last absorb's kernel time
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p->ev[2], p->ev[3]) == hipSuccess) p->kernel_ms += ms;
+    p->absorb_pending = false;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t lc_part_create(int32_t device, int32_t model_kind, int64_t init_value, int64_t n,
+                       const int64_t* index, const int32_t* process, const int8_t* type, const int8_t* f,
+                       const int64_t* v0, const int64_t* v1, const int8_t* vflags, int32_t rank,
+                       int32_t world, int32_t capacity_log2, lc_part** out, char* err, int32_t err_len) {
+  if (!out) return LC_E_ARG;
+  *out = nullptr;
+  if (model_kind != LC_MODEL_CAS_REGISTER) {
+    set_msg(err, err_len, "the partitioned search runs cas-register histories (counter: lc_check / bounds)");
+    return LC_E_ARG;
+  }
+  if (world < 1 || world > PW_MAX || rank < 0 || rank >= world) {
+    set_msg(err, err_len, "rank %d / world %d out of range (world <= %d)", rank, world, PW_MAX);
+    return LC_E_ARG;
+  }
+  if (n < 0 || (n > 0 && (!process || !type || !f || !v0 || !v1 || !vflags))) {
+    set_msg(err, err_len, "bad history arrays");
+    return LC_E_ARG;
+  }
+  if (capacity_log2 <= 0) capacity_log2 = 22;
+  if (capacity_log2 < 10 || capacity_log2 > 26) {
+    set_msg(err, err_len, "capacity_log2 %d out of [10, 26]", capacity_log2);
+    return LC_E_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    set_msg(err, err_len, "no HIP device visible (the checker has no CPU fallback)");
+    return LC_E_DEVICE;
+  }
+  if (device < 0 || device >= ndev) {
+    set_msg(err, err_len, "device %d out of range", device);
+    return LC_E_ARG;
+  }
+  auto p = std::make_unique<lc_part>();
+  p->device = device;
+  p->rank = rank;
+  p->world = world;
+  const int64_t off[2] = {0, n};
+  HistArrays a{n, index, process, type, f, v0, v1, vflags};
+  encode(model_kind, init_value, 1, off, a, p->enc);
+  p->mask_bits = std::max(1, p->enc.live_max[0]);
+  p->state_bits = bits_of(p->enc.n_states[0]);
+  if (!p->enc.err[0] && (p->mask_bits > PS_MAX || p->mask_bits + p->state_bits > KEY_BITS)) {
+    p->enc.err[0] = LC_H_WIDE;
+    p->enc.errmsg[0] = "pending ops + state bits exceed the 48-bit partitioned key";
+  }
+  PT_TRY(hipSetDevice(device));
+  p->slog = capacity_log2 + 1;  // tables at most half full
+  p->list_cap = 1ull << capacity_log2;
+  p->seg_cap = std::max<uint64_t>(1024, (p->list_cap >> 2) / (uint64_t)world);
+  const size_t tb = sizeof(uint64_t) << p->slog, lb = sizeof(uint64_t) * p->list_cap;
+  PT_TRY(hipMalloc(&p->S, tb));
+  PT_TRY(hipMalloc(&p->O, tb));
+  PT_TRY(hipMemset(p->S, 0, tb));
+  PT_TRY(hipMemset(p->O, 0, tb));
+  PT_TRY(hipMalloc(&p->F, lb));
+  PT_TRY(hipMalloc(&p->OUTL, lb));
+  PT_TRY(hipMalloc(&p->Lb[0], lb));
+  PT_TRY(hipMalloc(&p->Lb[1], lb));
+  PT_TRY(hipMalloc(&p->stage, sizeof(uint64_t) * p->seg_cap * (uint64_t)world));
+  PT_TRY(hipMalloc(&p->ctl, sizeof(PartCtl)));
+  PT_TRY(hipHostMalloc(&p->hctl, sizeof(PartCtl), hipHostMallocDefault));
+  PT_TRY(hipMemset(p->ctl, 0, sizeof(PartCtl)));
+  hipDeviceProp_t prop;
+  PT_TRY(hipGetDeviceProperties(&prop, device));
+  p->grid = prop.multiProcessorCount * 8;
+  for (hipEvent_t& e : p->ev) PT_TRY(hipEventCreate(&e));
+  // the initial config (nil, nothing linearized) = key 0 lives on rank 0
+  if (rank == 0) {
+    const uint64_t zero = 0;
+    const unsigned long long one = 1;
+    PT_TRY(hipMemcpy(p->F, &zero, sizeof zero, hipMemcpyHostToDevice));
+    PT_TRY(hipMemcpy(&p->ctl->fcount, &one, sizeof one, hipMemcpyHostToDevice));
+  }
+  *out = p.release();
+  return 0;
+}
+
+/* info[0] = RETURN steps, [1] history error (LC_H_*), [2] mask bits, [3] state bits,
+ * [4] invocations (ops), [5] list capacity, [6] kernel time so far (ns, HIP events),
+ * [7] algorithmic HBM bytes so far */
+int32_t lc_part_info(lc_part* p, int64_t* info, int32_t n) {
+  if (!p || !info) return LC_E_ARG;
+  const int64_t v[8] = {p->enc.n_steps(0), p->enc.err[0], p->mask_bits, p->state_bits, p->enc.n_ops[0],
+                        (int64_t)p->list_cap, (int64_t)(p->kernel_ms * 1e6), (int64_t)p->alg_bytes};
+  for (int i = 0; i < n && i < 8; ++i) info[i] = v[i];
+  return 0;
+}
+
+/* Begin RETURN step t (steps run in order 0, 1, ...): applies its invocations and makes the
+ * frontier F the level-0 list. */
+int32_t lc_part_step_begin(lc_part* p, int64_t t, void* stream, char* err, int32_t err_len) {
+  if (!p || t != p->t + 1 || t >= p->enc.n_steps(0) || p->enc.err[0]) {
+    set_msg(err, err_len, "step %lld out of order or history not searchable", (long long)t);
+    return LC_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  PT_TRY(hipSetDevice(p->device));
+  const Encoded& e = p->enc;
+  for (int64_t q = e.inv_off[t]; q < e.inv_off[t + 1]; ++q) {
+    const int k = e.inv_slot[q];
+    p->args.ops[k] = ((uint64_t)(uint32_t)(int32_t)e.inv_b[q] << 32) | (uint64_t)(uint32_t)(int32_t)e.inv_a[q];
+    p->live |= 1ull << k;
+  }
+  const int j = e.step_slot[t];
+  p->args.live = p->live;
+  p->args.bitj = 1ull << j;
+  p->args.mask_bits = p->mask_bits;
+  p->args.world = p->world;
+  p->args.rank = p->rank;
+  p->wd = (uint32_t)(64 - __builtin_clzll(p->live));
+  if (++p->epoch > EPOCH_MAX) {  // epochs wrapped: clear both sets once
+    PT_TRY(hipMemsetAsync(p->S, 0, sizeof(uint64_t) << p->slog, s));
+    PT_TRY(hipMemsetAsync(p->O, 0, sizeof(uint64_t) << p->slog, s));
+    p->epoch = 1;
+  }
+  PT_TRY(hipMemsetAsync(&p->ctl->ocount, 0, sizeof(unsigned long long), s));
+  PT_TRY(hipMemsetAsync(&p->ctl->scount, 0, sizeof(unsigned long long), s));
+  p->t = t;
+  p->level = 0;
+  p->cur = 0;
+  return 0;
+}
+
+/* Expand this rank's current level list. send_counts[d] = candidates for rank d. */
+int32_t lc_part_expand(lc_part* p, void* stream, int64_t* send_counts, char* err, int32_t err_len) {
+  if (!p || !send_counts || p->t < 0) return LC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  PT_TRY(hipSetDevice(p->device));
+  const uint64_t* list = p->level == 0 ? p->F : p->Lb[p->cur];
+  const unsigned long long* cnt = p->level == 0 ? &p->ctl->fcount : &p->ctl->lc[p->cur];
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    PT_TRY(hipMemsetAsync(p->ctl->cnt, 0, sizeof(p->ctl->cnt), s));
+    PT_TRY(hipEventRecord(p->ev[0], s));
+    hipLaunchKernelGGL(part_expand, dim3(p->grid), dim3(PT), 0, s, p->args, list, cnt, p->wd, p->stage,
+                       p->seg_cap, p->ctl);
+    PT_TRY(hipGetLastError());
+    PT_TRY(hipEventRecord(p->ev[1], s));
+    int rc = part_read_ctl(p, s, err, err_len);
+    if (rc) return rc;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p->ev[0], p->ev[1]) == hipSuccess) p->kernel_ms += ms;
+    uint64_t mx = 0;
+    for (int d = 0; d < p->world; ++d) mx = std::max<uint64_t>(mx, p->hctl->cnt[d]);
+    if (mx <= p->seg_cap) break;
+    uint64_t cap = p->seg_cap;
+    while (cap < mx) cap <<= 1;
+    PT_TRY(hipFree(p->stage));
+    p->stage = nullptr;
+    PT_TRY(hipMalloc(&p->stage, sizeof(uint64_t) * cap * (uint64_t)p->world));
+    p->seg_cap = cap;
+  }
+  if (p->hctl->flags & PF_OVERFLOW) {
+    set_msg(err, err_len, "frontier exceeded the partition capacity (LC_H_CAPACITY)");
+    return LC_H_CAPACITY;
+  }
+  const uint64_t listed = p->level == 0 ? p->hctl->fcount : p->hctl->lc[p->cur];
+  uint64_t cand = 0;
+  for (int d = 0; d < p->world; ++d) send_counts[d] = (int64_t)p->hctl->cnt[d], cand += p->hctl->cnt[d];
+  // read the list (8 B / config), write each candidate (8 B)
+  p->alg_bytes += 8.0 * (double)listed + 8.0 * (double)cand;
+  return 0;
+}
+
+/* Copy the last expand's candidates into dst (device memory), contiguous by destination rank
+ * in rank order (an all-to-all's input). dst_cap in entries. */
+int32_t lc_part_pack(lc_part* p, void* stream, void* dst, int64_t dst_cap, char* err, int32_t err_len) {
+  if (!p || (!dst && dst_cap > 0)) return LC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  uint64_t tot = 0;
+  for (int d = 0; d < p->world; ++d) tot += p->hctl->cnt[d];
+  if ((int64_t)tot > dst_cap) {
+    set_msg(err, err_len, "pack buffer holds %lld entries, %llu needed", (long long)dst_cap,
+            (unsigned long long)tot);
+    return LC_E_ARG;
+  }
+  PT_TRY(hipSetDevice(p->device));
+  uint64_t o = 0;
+  for (int d = 0; d < p->world; ++d) {
+    const uint64_t c = p->hctl->cnt[d];
+    if (c)
+      PT_TRY(hipMemcpyAsync((uint64_t*)dst + o, p->stage + (uint64_t)d * p->seg_cap, c * sizeof(uint64_t),
+                            hipMemcpyDeviceToDevice, s));
+    o += c;
+  }
+  return 0;
+}
+
+/* Absorb n candidates this rank owns (device memory; NULL = this rank's own staged segment,
+ * for world 1). Ends the level. */
+int32_t lc_part_absorb(lc_part* p, void* stream, const void* recv, int64_t n, char* err, int32_t err_len) {
+  if (!p || n < 0 || p->t < 0) return LC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  PT_TRY(hipSetDevice(p->device));
+  const uint64_t* src = (const uint64_t*)recv;
+  if (!src && n > 0) {
+    if (p->world != 1 || (uint64_t)n != p->hctl->cnt[0]) {
+      set_msg(err, err_len, "NULL recv needs world 1 and n = the staged count");
+      return LC_E_ARG;
+    }
+    src = p->stage;
+  }
+  const int nxt = p->level == 0 ? 0 : p->cur ^ 1;
+  PT_TRY(hipMemsetAsync(&p->ctl->lc[nxt], 0, sizeof(unsigned long long), s));
+  if (n > 0) {
+    const uint64_t tmask = (1ull << p->slog) - 1;
+    const int grid = (int)std::min<int64_t>(p->grid, (n + PT - 1) / PT);
+    PT_TRY(hipEventRecord(p->ev[2], s));
+    hipLaunchKernelGGL(part_absorb, dim3(grid), dim3(PT), 0, s, src, (uint64_t)n, p->args.bitj, p->S, tmask, p->O,
+                       tmask, (uint64_t)p->epoch, p->Lb[nxt], &p->ctl->lc[nxt], p->OUTL, p->list_cap, p->ctl);
+    PT_TRY(hipGetLastError());
+    PT_TRY(hipEventRecord(p->ev[3], s));
+    p->absorb_pending = true;
+    // read each candidate (8 B) and probe its hash word (8 B read + CAS); survivors are
+    // counted in the next expand's list read
+    p->alg_bytes += 16.0 * (double)n;
+  }
+  p->cur = nxt;
+  p->level++;
+  return 0;
+}
+
+/* End the step: F = OUT. *out_count = this rank's frontier size (sum over ranks = 0 =>
+ * not linearizable at this step). */
+int32_t lc_part_step_end(lc_part* p, void* stream, int64_t* out_count, char* err, int32_t err_len) {
+  if (!p || !out_count || p->t < 0) return LC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  PT_TRY(hipSetDevice(p->device));
+  PT_TRY(hipMemcpyAsync(&p->ctl->fcount, &p->ctl->ocount, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
+  int rc = part_read_ctl(p, s, err, err_len);
+  if (rc) return rc;
+  if (p->hctl->flags & PF_OVERFLOW) {
+    set_msg(err, err_len, "frontier exceeded the partition capacity (LC_H_CAPACITY)");
+    return LC_H_CAPACITY;
+  }
+  std::swap(p->F, p->OUTL);
+  p->live &= ~p->args.bitj;
+  *out_count = (int64_t)p->hctl->ocount;
+  return 0;
+}
+
+/* This rank's explored count so far, and the :index triple of step t (failure reports):
+ * out[0] explored, out[1] :index of step t's :ok completion, out[2] of its invocation,
+ * out[3] of the previous step's completion (-1 at t = 0). */
+int32_t lc_part_results(lc_part* p, int64_t t, void* stream, int64_t* out4, char* err, int32_t err_len) {
+  if (!p || !out4) return LC_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  PT_TRY(hipSetDevice(p->device));
+  int rc = part_read_ctl(p, s, err, err_len);
+  if (rc) return rc;
+  out4[0] = (int64_t)p->hctl->explored;
+  const int64_t ns = p->enc.n_steps(0);
+  out4[1] = (t >= 0 && t < ns) ? p->enc.step_cmp_idx[t] : -1;
+  out4[2] = (t >= 0 && t < ns) ? p->enc.step_inv_idx[t] : -1;
+  out4[3] = (t > 0 && t <= ns) ? p->enc.step_cmp_idx[t - 1] : -1;
+  return 0;
+}
+
+void lc_part_destroy(lc_part* p) { delete p; }
+
+}  // extern "C"

@@ -15,7 +15,9 @@ LIB_PATH = os.path.join(HERE, "liblincheck.so")
 EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_failure_configs",
            "lc_counter_bounds", "lc_plan_create", "lc_plan_run", "lc_plan_results",
            "lc_plan_stats", "lc_plan_destroy", "lc_bounds_plan_create", "lc_bounds_plan_sums",
-           "lc_bounds_plan_run", "lc_bounds_plan_destroy")
+           "lc_bounds_plan_run", "lc_bounds_plan_destroy", "lc_part_create", "lc_part_info",
+           "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
+           "lc_part_step_end", "lc_part_results", "lc_part_destroy")
 STATS_N = 20
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
@@ -69,6 +71,25 @@ def load():
     L.lc_bounds_plan_run.restype = C.c_int32
     L.lc_bounds_plan_destroy.argtypes = [P]
     L.lc_bounds_plan_destroy.restype = None
+    L.lc_part_create.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.c_int64] + [P] * 7 + \
+        [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p), C.c_char_p, C.c_int32]
+    L.lc_part_create.restype = C.c_int32
+    L.lc_part_info.argtypes = [P, P, C.c_int32]
+    L.lc_part_info.restype = C.c_int32
+    L.lc_part_step_begin.argtypes = [P, C.c_int64, P, C.c_char_p, C.c_int32]
+    L.lc_part_step_begin.restype = C.c_int32
+    L.lc_part_expand.argtypes = [P, P, P, C.c_char_p, C.c_int32]
+    L.lc_part_expand.restype = C.c_int32
+    L.lc_part_pack.argtypes = [P, P, P, C.c_int64, C.c_char_p, C.c_int32]
+    L.lc_part_pack.restype = C.c_int32
+    L.lc_part_absorb.argtypes = [P, P, P, C.c_int64, C.c_char_p, C.c_int32]
+    L.lc_part_absorb.restype = C.c_int32
+    L.lc_part_step_end.argtypes = [P, P, P, C.c_char_p, C.c_int32]
+    L.lc_part_step_end.restype = C.c_int32
+    L.lc_part_results.argtypes = [P, C.c_int64, P, P, C.c_char_p, C.c_int32]
+    L.lc_part_results.restype = C.c_int32
+    L.lc_part_destroy.argtypes = [P]
+    L.lc_part_destroy.restype = None
     if L.lc_abi_version() != 1:
         raise LincheckError("ABI version mismatch")
     _lib = L
@@ -236,3 +257,84 @@ class BoundsPlan:
             self.close()
         except Exception:
             pass
+
+
+class PartPlan:
+    """One rank's part of a single cas-register history whose frontier is partitioned over
+    `world` ranks by config hash (lc_part_*, SURVEY §8(e) axis 2). Driven level by level by
+    lincheck.partition.search, which runs the collectives. Buffers are torch tensors on the
+    plan's device (or None where the C-ABI allows NULL); `stream` is a hipStream_t handle."""
+
+    H_CAPACITY = -7
+
+    def __init__(self, h, hist: int = 0, rank: int = 0, world: int = 1, device: int = 0,
+                 capacity_log2: int = 0):
+        L = load()
+        self._L = L
+        self.rank, self.world = rank, world
+        b, e = int(h.off[hist]), int(h.off[hist + 1])
+        keep = [np.ascontiguousarray(a[b:e]) for a in
+                (h.index, h.process, h.type, h.f, h.v0, h.v1, h.vflags)]
+        handle = C.c_void_p()
+        buf = _errbuf()
+        rc = L.lc_part_create(device, 1, 0, e - b, *[_p(a) for a in keep], rank, world,
+                              capacity_log2, C.byref(handle), buf, len(buf))
+        _raise(rc, buf, "lc_part_create")
+        self._h = handle
+        info = np.zeros(6, np.int64)
+        L.lc_part_info(self._h, _p(info), 6)
+        self.n_steps, self.err, self.mask_bits, self.state_bits, self.n_ops, self.list_cap = \
+            (int(x) for x in info)
+        self._counts = np.zeros(world, np.int64)
+
+    def stats(self):
+        """kernel time (ms, HIP events on the caller's stream) and algorithmic HBM bytes so far"""
+        info = np.zeros(8, np.int64)
+        self._L.lc_part_info(self._h, _p(info), 8)
+        return {"kernel_ms": float(info[6]) / 1e6, "alg_bytes": float(info[7])}
+
+    def _call(self, fn, *args):
+        buf = _errbuf()
+        rc = fn(self._h, *args, buf, len(buf))
+        if rc == self.H_CAPACITY:
+            raise CapacityError(buf.value.decode(errors="replace"))
+        _raise(rc, buf, fn.__name__)
+
+    def step_begin(self, t: int, stream=None):
+        self._call(self._L.lc_part_step_begin, t, stream)
+
+    def expand(self, stream=None):
+        self._call(self._L.lc_part_expand, stream, _p(self._counts))
+        return self._counts.copy()
+
+    def pack(self, dst, stream=None):
+        self._call(self._L.lc_part_pack, stream, dst.data_ptr(), dst.numel())
+
+    def absorb(self, recv, n: int, stream=None):
+        self._call(self._L.lc_part_absorb, stream, None if recv is None else recv.data_ptr(), n)
+
+    def step_end(self, stream=None) -> int:
+        out = np.zeros(1, np.int64)
+        self._call(self._L.lc_part_step_end, stream, _p(out))
+        return int(out[0])
+
+    def results(self, t: int, stream=None):
+        """-> (this rank's explored, fail :index, its invocation's :index, previous :ok's)"""
+        out = np.zeros(4, np.int64)
+        self._call(self._L.lc_part_results, t, stream, _p(out))
+        return tuple(int(x) for x in out)
+
+    def close(self):
+        if self._h:
+            self._L.lc_part_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class CapacityError(LincheckError):
+    """The frontier outgrew the plan's capacity (LC_H_CAPACITY: verdict :unknown)."""

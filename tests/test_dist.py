@@ -66,3 +66,69 @@ def test_shards_partition(n, world):
         assert e0 == b1 and b0 <= e0
     sizes = [e - b for b, e in spans]
     assert max(sizes) - min(sizes) <= 1
+
+
+# ---- axis 2: one history, frontier partitioned over ranks (lincheck.partition) ----------
+# The level protocol (count all-gather, all-to-all of candidates, frontier all-reduce) runs
+# under gloo with a numpy stand-in for the per-rank HIP plan (tests/part_mock.py); the HIP
+# plan itself runs the same driver in test_gpu.py.
+
+def _part_histories():
+    from lincheck import synth
+    hs = [synth.gen_register_keys(1, 120, 5, 0.02, config_id=7, key0=k) for k in range(3)]
+    hs += [synth.gen_register_keys(1, 120, 5, 0.02, config_id=7, key0=k, invalid_keys=(k,))
+           for k in (7, 17)]
+    return hs
+
+
+def _part_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lincheck import partition
+        from part_mock import MockPartPlan
+        out = []
+        for h in _part_histories():
+            r = partition.search(MockPartPlan(h, rank=rank, world=world), tdist, "cpu", None)
+            out.append((r["valid"], r["fail_idx"], r["fail_inv"], r["prev_ok"], r["explored"]))
+        q.put((rank, out))
+    finally:
+        tdist.destroy_process_group()
+
+
+def _oracle_rows():
+    import oracle
+    rows = []
+    for h in _part_histories():
+        e = oracle.check_one("cas-register", h)
+        rows.append((e["valid"], e["fail_idx"] if e["valid"] == 0 else -1,
+                     e["fail_inv_idx"] if e["valid"] == 0 else -1,
+                     e["prev_ok_idx"] if e["valid"] == 0 else -1, e["explored"]))
+    return rows
+
+
+def test_partitioned_search_world1_matches_oracle():
+    from lincheck import partition
+    from part_mock import MockPartPlan
+    exp = _oracle_rows()
+    assert any(r[0] == 0 for r in exp) and any(r[0] == 1 for r in exp)
+    for h, e in zip(_part_histories(), exp):
+        r = partition.search(MockPartPlan(h), None, "cpu", None)
+        assert (r["valid"], r["fail_idx"], r["fail_inv"], r["prev_ok"], r["explored"]) == e
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_search_gloo_matches_oracle(world):
+    exp = _oracle_rows()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_part_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert [tuple(x) for x in got[r]] == exp, (r, got[r], exp)

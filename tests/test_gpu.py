@@ -453,3 +453,80 @@ def test_gpu_cell_overflow_buckets(monkeypatch):
     exp = oracle.check_many("cas-register", h)
     for k in range(h.n_hist):
         _cmp(g, exp[k], k, "overflow")
+
+
+# ---- axis 2: one history, frontier partitioned by config hash (csrc/part.hip) -----------
+
+def _part_row(r):
+    return (r["valid"], r["fail_idx"], r["fail_inv"], r["prev_ok"], r["explored"])
+
+
+def _oracle_part_row(h):
+    e = oracle.check_one("cas-register", h)
+    bad = e["valid"] == 0
+    return (e["valid"], e["fail_idx"] if bad else -1, e["fail_inv_idx"] if bad else -1,
+            e["prev_ok_idx"] if bad else -1, e["explored"])
+
+
+def _part_cases():
+    hs = [synth.gen_register_keys(1, 300, 5, 0.02, config_id=7, key0=k) for k in range(4)]
+    hs += [synth.gen_register_keys(1, 120, 5, 0.02, config_id=7, key0=k, invalid_keys=(k,))
+           for k in (7, 8, 15, 17, 28)]
+    hs.append(synth.gen_config("c2", scale=0.1))
+    return hs
+
+
+def test_gpu_partitioned_world1_vs_oracle():
+    from lincheck import partition
+    for i, h in enumerate(_part_cases()):
+        r = partition.check_partitioned(h)
+        assert _part_row(r) == _oracle_part_row(h), (i, r)
+
+
+def test_gpu_partitioned_matches_dense_on_c2_slice():
+    from lincheck import partition
+    h = synth.gen_config("c2", scale=0.3)
+    r = partition.check_partitioned(h)
+    g = _lib.check(1, 0, h)
+    assert (r["valid"], r["explored"]) == (int(g["valid"][0]), int(g["explored"][0]))
+
+
+def test_gpu_partitioned_capacity_is_unknown():
+    from lincheck import partition
+    h = synth.gen_config("c2", scale=0.1)
+    r = partition.check_partitioned(h, capacity_log2=10)
+    assert r["valid"] == 2 and r["err"] == -7
+
+
+def _gpu_part_worker(rank, world, port, q):
+    import torch.distributed as tdist
+    from lincheck import partition
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, [_part_row(partition.check_partitioned(h, tdist=tdist, device_index=0))
+                      for h in _part_cases()[3:]]))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_gpu_partitioned_two_ranks_one_gpu_gloo():
+    """Two ranks (processes) on cuda:0, candidates exchanged through gloo: the HIP plan's
+    routing, DIRECT returns and per-rank dedup give the oracle's answers."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_part_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=100) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    exp = [_oracle_part_row(h) for h in _part_cases()[3:]]
+    for r in range(2):
+        assert [tuple(x) for x in got[r]] == exp, (r, got[r], exp)
