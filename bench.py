@@ -185,12 +185,14 @@ def bench_partition(args, rank, world, dist, barrier_sync):
     tdist = dist[1] if dist else None
     h = synth.gen_config(args.workload, scale=args.scale)
     local = int(os.environ.get("LOCAL_RANK", 0))
+    # per-rank lists of 2^cap configs; C4's widest closures need 2^25 on one rank
+    cap = args.capacity_log2 or (25 if args.workload == "c4" else 22)
     runs = []
     for i in range(args.warmup + args.steps):
         if i == args.warmup:
             barrier_sync()
             t0 = time.perf_counter()
-        r = partition.check_partitioned(h, tdist=tdist, device_index=local)
+        r = partition.check_partitioned(h, tdist=tdist, device_index=local, capacity_log2=cap)
         if i >= args.warmup:
             runs.append(r)
     barrier_sync()
@@ -246,6 +248,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--partition", action="store_true",
                     help="axis 2: one history (c2/c4) with its frontier partitioned over ranks")
+    ap.add_argument("--capacity-log2", type=int, default=0, help="--partition: per-rank capacity")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC passes (or absent)")
     args = ap.parse_args()

@@ -51,12 +51,10 @@ enum : int { PF_OVERFLOW = 1 };
 struct PartCtl {
   unsigned long long cnt[PW_MAX];  // candidates per destination (this level)
   unsigned long long lc[2];        // level lists (count)
-  unsigned long long fcount;       // frontier F
-  unsigned long long ocount;       // OUT list
-  unsigned long long scount;       // S inserts this step
+  unsigned long long oc[2];        // frontier F / OUT list, by step parity (F = oc[sp ^ 1])
   unsigned long long explored;     // all steps
   unsigned long long flags;
-  unsigned long long pad[5];
+  unsigned long long pad[6];
 };
 
 struct StepArgs {
@@ -70,17 +68,18 @@ __device__ __forceinline__ uint32_t owner_of(uint64_t k, uint32_t world) {
   return (uint32_t)(((mix64(k) >> 32) * (uint64_t)world) >> 32);
 }
 
-// global-counter append: lanes with `pred` get distinct positions, one atomic per wave
-__device__ __forceinline__ unsigned long long wave_append_g(unsigned long long* counter, bool pred) {
+// Block-aggregated append, step 1: every wave adds its ballot count of `pred` to the LDS
+// counter and gets its lanes' offsets within the block (one LDS atomic per wave).
+__device__ __forceinline__ uint32_t block_slot(uint32_t* s_counter, bool pred) {
   const unsigned long long m = __ballot(pred);
   if (m == 0) return 0;
   const int lane = __lane_id();
   const int leader = __ffsll((long long)m) - 1;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(m));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(s_counter, (uint32_t)__popcll(m));
   base = __shfl(base, leader, 64);
   const unsigned long long below = lane ? (m & ((~0ull) >> (64 - lane))) : 0ull;
-  return base + (unsigned long long)__popcll(below);
+  return base + (uint32_t)__popcll(below);
 }
 
 // insert key (< 2^48) into an epoch-tagged open-addressing set; 1 = new, 0 = present
@@ -106,94 +105,167 @@ __device__ __forceinline__ int set_insert(uint64_t* T, uint64_t tmask, uint64_t 
   return 0;
 }
 
-// Expand: thread per (config, slot) pair of the list; candidates staged per destination
-// ([world][seg_cap]); counts may exceed seg_cap (the host then grows the staging and re-runs).
+// One pending op k stepped from config c (cas-register), or c's DIRECT return (k = 0 only)
+struct Cand {
+  bool has;
+  uint32_t dst;
+  uint64_t out;
+};
+__device__ __forceinline__ Cand candidate(const StepArgs& a, uint64_t c, bool valid, int k, uint64_t mmask) {
+  Cand r{false, 0u, 0ull};
+  if (!valid) return r;
+  uint64_t route = 0;
+  if (c & a.bitj) {  // already linearized the returning op: its image goes straight to OUT
+    if (k != 0) return r;
+    route = c & ~a.bitj;
+    r.out = route | DIRECT;
+    r.has = true;
+  } else if (((a.live >> k) & 1) && !((c >> k) & 1)) {
+    const uint64_t op = a.ops[k];
+    const int32_t ea = (int32_t)(uint32_t)op, nb = (int32_t)(uint32_t)(op >> 32);
+    const int64_t st = (int64_t)(c >> a.mask_bits);
+    if (ea == -1 || ea == st) {
+      const uint64_t ns = nb < 0 ? (uint64_t)st : (uint64_t)nb;
+      r.out = (ns << a.mask_bits) | (c & mmask) | (1ull << k);
+      route = r.out & ~a.bitj;
+      r.has = true;
+    }
+  }
+  if (r.has) r.dst = owner_of(route, (uint32_t)a.world);
+  return r;
+}
+
+// Expand: thread per config of the list, its candidates over the pending slots staged per
+// destination ([world][seg_cap]). Positions are reserved per block (LDS counts, then one
+// global atomic per destination per block pass) and handed out per wave (ballots), so the
+// global counters see ~n/256 atomics, not one per wave and slot. Counts may exceed seg_cap
+// (the host then grows the staging and re-runs).
 __global__ void __launch_bounds__(PT) part_expand(StepArgs a, const uint64_t* __restrict__ list,
                                                   const unsigned long long* __restrict__ count, uint32_t wd,
-                                                  uint64_t* __restrict__ stage, uint64_t seg_cap, PartCtl* ctl) {
-  const uint32_t n = (uint32_t)count[0] * wd;  // < 2^32: list_cap <= 2^26, wd <= 48
+                                                  uint64_t* __restrict__ stage, uint64_t seg_cap, PartCtl* ctl,
+                                                  unsigned long long* zero_a, unsigned long long* zero_b) {
+  __shared__ uint32_t s_cnt[PW_MAX];
+  // counters the following absorb fills (the next list's, and OUT's at level 0): no memset
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *zero_a = 0;
+    if (zero_b) *zero_b = 0;
+  }
+  __shared__ unsigned long long s_base[PW_MAX];
+  const uint64_t n = count[0];
   const uint64_t mmask = (1ull << a.mask_bits) - 1;
-  const uint32_t stride = gridDim.x * PT;
-  for (uint32_t it = blockIdx.x * PT; it < n; it += stride) {  // block-uniform trip count
-    const uint32_t i = it + threadIdx.x;
-    bool has = false;
-    uint64_t out = 0, route = 0;
-    if (i < n) {
-      const uint32_t ci = i / wd;
-      const uint64_t c = list[ci];
-      const int k = (int)(i - ci * wd);
-      if (c & a.bitj) {  // already linearized the returning op: its image goes straight to OUT
-        if (k == 0) {
-          route = c & ~a.bitj;
-          out = route | DIRECT;
-          has = true;
-        }
-      } else if (((a.live >> k) & 1) && !((c >> k) & 1)) {
-        const uint64_t op = a.ops[k];
-        const int32_t ea = (int32_t)(uint32_t)op, nb = (int32_t)(uint32_t)(op >> 32);
-        const int64_t st = (int64_t)(c >> a.mask_bits);
-        if (ea == -1 || ea == st) {
-          const uint64_t ns = nb < 0 ? (uint64_t)st : (uint64_t)nb;
-          out = (ns << a.mask_bits) | (c & mmask) | (1ull << k);
-          route = out & ~a.bitj;
-          has = true;
+  const uint64_t stride = (uint64_t)gridDim.x * PT;
+  const int W = a.world;
+  for (uint64_t it = (uint64_t)blockIdx.x * PT; it < n; it += stride) {  // block-uniform trip count
+    const uint64_t i = it + threadIdx.x;
+    const bool valid = i < n;
+    const uint64_t c = valid ? list[i] : 0ull;
+    if (threadIdx.x < (unsigned)W) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    // pass 1: this block's candidates per destination
+    for (int k = 0; k < (int)wd; ++k) {
+      const Cand q = candidate(a, c, valid, k, mmask);
+      for (int d = 0; d < W; ++d) {
+        const unsigned long long m = __ballot(q.has && q.dst == (uint32_t)d);
+        if (m && __lane_id() == 0) atomicAdd(&s_cnt[d], (uint32_t)__popcll(m));
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)W) {
+      const uint32_t cnt = s_cnt[threadIdx.x];
+      s_base[threadIdx.x] = cnt ? atomicAdd(&ctl->cnt[threadIdx.x], (unsigned long long)cnt) : 0ull;
+      s_cnt[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    // pass 2: the same candidates, written at the block's reserved positions
+    for (int k = 0; k < (int)wd; ++k) {
+      const Cand q = candidate(a, c, valid, k, mmask);
+      for (int d = 0; d < W; ++d) {
+        const bool mine = q.has && q.dst == (uint32_t)d;
+        const uint32_t off = block_slot(&s_cnt[d], mine);
+        if (mine) {
+          const unsigned long long pos = s_base[d] + off;
+          if (pos < seg_cap) stage[(uint64_t)d * seg_cap + pos] = q.out;
         }
       }
     }
-    const uint32_t dst = has ? owner_of(route, (uint32_t)a.world) : 0u;
-    for (int d = 0; d < a.world; ++d) {
-      const unsigned long long pos = wave_append_g(&ctl->cnt[d], has && dst == (uint32_t)d);
-      if (has && dst == (uint32_t)d && pos < seg_cap) stage[(uint64_t)d * seg_cap + pos] = out;
-    }
+    __syncthreads();  // s_cnt / s_base are reused by the next pass
   }
 }
 
-// Absorb the candidates this rank owns: dedup into S / OUT, compact the survivors.
+// Absorb the candidates this rank owns: dedup into S / OUT, compact the survivors. Each thread
+// takes AB items per block pass (independent hash probes in flight); list positions are
+// reserved per block (LDS counts, one global atomic per list per pass).
+constexpr int AB = 4;
 __global__ void __launch_bounds__(PT) part_absorb(const uint64_t* __restrict__ recv, uint64_t n, uint64_t bitj,
                                                   uint64_t* S, uint64_t smask, uint64_t* O, uint64_t omask,
                                                   uint64_t ep, uint64_t* __restrict__ next,
-                                                  unsigned long long* next_count, uint64_t* __restrict__ outl,
-                                                  uint64_t list_cap, PartCtl* ctl) {
-  const uint64_t stride = (uint64_t)gridDim.x * PT;
+                                                  unsigned long long* next_count, unsigned long long* out_count,
+                                                  uint64_t* __restrict__ outl, uint64_t list_cap, PartCtl* ctl,
+                                                  int world) {
+  __shared__ uint32_t s_cnt[2];
+  // the last expand's per-destination counts (already read by the host) start the next one at 0
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)world) ctl->cnt[threadIdx.x] = 0;
+  __shared__ unsigned long long s_base[2];
+  const uint64_t stride = (uint64_t)gridDim.x * PT * AB;
   unsigned long long expl = 0;
-  for (uint64_t it = (uint64_t)blockIdx.x * PT; it < n; it += stride) {
-    const uint64_t i = it + threadIdx.x;
-    bool news = false, newo = false, nl = false;
-    uint64_t key = 0, okey = 0;
-    if (i < n) {
-      key = recv[i];
-      if (key & DIRECT) {
-        okey = key & ~DIRECT;
-        newo = set_insert(O, omask, okey, ep, &ctl->flags);
+  for (uint64_t it = (uint64_t)blockIdx.x * PT * AB; it < n; it += stride) {
+    uint64_t key[AB], okey[AB];
+    bool news[AB], newo[AB];
+#pragma unroll
+    for (int u = 0; u < AB; ++u) {
+      const uint64_t i = it + (uint64_t)u * PT + threadIdx.x;
+      key[u] = i < n ? recv[i] : 0ull;
+      news[u] = newo[u] = false;
+      okey[u] = 0;
+    }
+#pragma unroll
+    for (int u = 0; u < AB; ++u) {
+      if (it + (uint64_t)u * PT + threadIdx.x >= n) continue;
+      if (key[u] & DIRECT) {
+        okey[u] = key[u] & ~DIRECT;
+        newo[u] = set_insert(O, omask, okey[u], ep, &ctl->flags);
       } else {
-        news = set_insert(S, smask, key, ep, &ctl->flags);
-        if (news) {
-          if (key & bitj) {
-            okey = key & ~bitj;
-            newo = set_insert(O, omask, okey, ep, &ctl->flags);
-          } else {
-            nl = true;
-          }
+        news[u] = set_insert(S, smask, key[u], ep, &ctl->flags);
+        if (news[u] && (key[u] & bitj)) {
+          okey[u] = key[u] & ~bitj;
+          newo[u] = set_insert(O, omask, okey[u], ep, &ctl->flags);
         }
       }
     }
-    expl += news;
-    const unsigned long long pn = wave_append_g(next_count, nl);
-    if (nl) {
-      if (pn < list_cap) next[pn] = key;
-      else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+    if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t pn[AB], po[AB];
+#pragma unroll
+    for (int u = 0; u < AB; ++u) {
+      const bool nl = news[u] && !(key[u] & bitj);
+      expl += news[u];
+      pn[u] = block_slot(&s_cnt[0], nl);
+      po[u] = block_slot(&s_cnt[1], newo[u]);
     }
-    const unsigned long long po = wave_append_g(&ctl->ocount, newo);
-    if (newo) {
-      if (po < list_cap) outl[po] = okey;
-      else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      const uint32_t cnt = s_cnt[threadIdx.x];
+      s_base[threadIdx.x] = cnt ? atomicAdd(threadIdx.x == 0 ? next_count : out_count, (unsigned long long)cnt)
+                                : 0ull;
     }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < AB; ++u) {
+      if (news[u] && !(key[u] & bitj)) {
+        const unsigned long long q = s_base[0] + pn[u];
+        if (q < list_cap) next[q] = key[u];
+        else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+      }
+      if (newo[u]) {
+        const unsigned long long q = s_base[1] + po[u];
+        if (q < list_cap) outl[q] = okey[u];
+        else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+      }
+    }
+    __syncthreads();  // s_cnt / s_base are reused by the next pass
   }
   for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
-  if (__lane_id() == 0 && expl) {
-    atomicAdd(&ctl->explored, expl);
-    atomicAdd(&ctl->scount, expl);
-  }
+  if (__lane_id() == 0 && expl) atomicAdd(&ctl->explored, expl);
 }
 
 void set_msg(char* err, int32_t len, const char* fmt, ...) {
@@ -235,7 +307,8 @@ struct lc_part {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool absorb_pending = false;
   double kernel_ms = 0, alg_bytes = 0;
-  uint64_t listed = 0;  // entries of the list the last expand read
+  int sp = 0;          // step parity: OUT count = ctl->oc[sp], F count = ctl->oc[sp ^ 1]
+  uint64_t ub = 1;      // upper bound of the next expand's list (grid sizing): |F| or the last absorb's n
   // step state
   int64_t t = -1;
   uint32_t epoch = 0;
@@ -352,7 +425,7 @@ int32_t lc_part_create(int32_t device, int32_t model_kind, int64_t init_value, i
     const uint64_t zero = 0;
     const unsigned long long one = 1;
     PT_TRY(hipMemcpy(p->F, &zero, sizeof zero, hipMemcpyHostToDevice));
-    PT_TRY(hipMemcpy(&p->ctl->fcount, &one, sizeof one, hipMemcpyHostToDevice));
+    PT_TRY(hipMemcpy(&p->ctl->oc[1], &one, sizeof one, hipMemcpyHostToDevice));
   }
   *out = p.release();
   return 0;
@@ -396,8 +469,6 @@ int32_t lc_part_step_begin(lc_part* p, int64_t t, void* stream, char* err, int32
     PT_TRY(hipMemsetAsync(p->O, 0, sizeof(uint64_t) << p->slog, s));
     p->epoch = 1;
   }
-  PT_TRY(hipMemsetAsync(&p->ctl->ocount, 0, sizeof(unsigned long long), s));
-  PT_TRY(hipMemsetAsync(&p->ctl->scount, 0, sizeof(unsigned long long), s));
   p->t = t;
   p->level = 0;
   p->cur = 0;
@@ -410,12 +481,16 @@ int32_t lc_part_expand(lc_part* p, void* stream, int64_t* send_counts, char* err
   hipStream_t s = (hipStream_t)stream;
   PT_TRY(hipSetDevice(p->device));
   const uint64_t* list = p->level == 0 ? p->F : p->Lb[p->cur];
-  const unsigned long long* cnt = p->level == 0 ? &p->ctl->fcount : &p->ctl->lc[p->cur];
+  const unsigned long long* cnt = p->level == 0 ? &p->ctl->oc[p->sp ^ 1] : &p->ctl->lc[p->cur];
+  // the list the following absorb appends to (see lc_part_absorb)
+  unsigned long long* next_cnt = &p->ctl->lc[p->level == 0 ? 0 : p->cur ^ 1];
+  unsigned long long* out_cnt = p->level == 0 ? &p->ctl->oc[p->sp] : nullptr;
   for (int attempt = 0; attempt < 2; ++attempt) {
-    PT_TRY(hipMemsetAsync(p->ctl->cnt, 0, sizeof(p->ctl->cnt), s));
+    if (attempt) PT_TRY(hipMemsetAsync(p->ctl->cnt, 0, sizeof(p->ctl->cnt), s));
     PT_TRY(hipEventRecord(p->ev[0], s));
-    hipLaunchKernelGGL(part_expand, dim3(p->grid), dim3(PT), 0, s, p->args, list, cnt, p->wd, p->stage,
-                       p->seg_cap, p->ctl);
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(p->grid, (p->ub + PT - 1) / PT));
+    hipLaunchKernelGGL(part_expand, dim3(grid), dim3(PT), 0, s, p->args, list, cnt, p->wd, p->stage,
+                       p->seg_cap, p->ctl, next_cnt, out_cnt);
     PT_TRY(hipGetLastError());
     PT_TRY(hipEventRecord(p->ev[1], s));
     int rc = part_read_ctl(p, s, err, err_len);
@@ -436,7 +511,7 @@ int32_t lc_part_expand(lc_part* p, void* stream, int64_t* send_counts, char* err
     set_msg(err, err_len, "frontier exceeded the partition capacity (LC_H_CAPACITY)");
     return LC_H_CAPACITY;
   }
-  const uint64_t listed = p->level == 0 ? p->hctl->fcount : p->hctl->lc[p->cur];
+  const uint64_t listed = p->level == 0 ? p->hctl->oc[p->sp ^ 1] : p->hctl->lc[p->cur];
   uint64_t cand = 0;
   for (int d = 0; d < p->world; ++d) send_counts[d] = (int64_t)p->hctl->cnt[d], cand += p->hctl->cnt[d];
   // read the list (8 B / config), write each candidate (8 B)
@@ -483,13 +558,15 @@ int32_t lc_part_absorb(lc_part* p, void* stream, const void* recv, int64_t n, ch
     src = p->stage;
   }
   const int nxt = p->level == 0 ? 0 : p->cur ^ 1;
-  PT_TRY(hipMemsetAsync(&p->ctl->lc[nxt], 0, sizeof(unsigned long long), s));
+  if (n == 0)  // no kernel to reset the expand counts (lc[nxt] was reset by the expand)
+    PT_TRY(hipMemsetAsync(p->ctl->cnt, 0, sizeof(p->ctl->cnt), s));
   if (n > 0) {
     const uint64_t tmask = (1ull << p->slog) - 1;
-    const int grid = (int)std::min<int64_t>(p->grid, (n + PT - 1) / PT);
+    const int grid = (int)std::min<int64_t>(p->grid, (n + PT * AB - 1) / (PT * AB));
     PT_TRY(hipEventRecord(p->ev[2], s));
     hipLaunchKernelGGL(part_absorb, dim3(grid), dim3(PT), 0, s, src, (uint64_t)n, p->args.bitj, p->S, tmask, p->O,
-                       tmask, (uint64_t)p->epoch, p->Lb[nxt], &p->ctl->lc[nxt], p->OUTL, p->list_cap, p->ctl);
+                       tmask, (uint64_t)p->epoch, p->Lb[nxt], &p->ctl->lc[nxt], &p->ctl->oc[p->sp], p->OUTL,
+                       p->list_cap, p->ctl, p->world);
     PT_TRY(hipGetLastError());
     PT_TRY(hipEventRecord(p->ev[3], s));
     p->absorb_pending = true;
@@ -499,6 +576,7 @@ int32_t lc_part_absorb(lc_part* p, void* stream, const void* recv, int64_t n, ch
   }
   p->cur = nxt;
   p->level++;
+  p->ub = (uint64_t)n;  // the next list holds at most the candidates absorbed here
   return 0;
 }
 
@@ -508,7 +586,6 @@ int32_t lc_part_step_end(lc_part* p, void* stream, int64_t* out_count, char* err
   if (!p || !out_count || p->t < 0) return LC_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   PT_TRY(hipSetDevice(p->device));
-  PT_TRY(hipMemcpyAsync(&p->ctl->fcount, &p->ctl->ocount, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
   int rc = part_read_ctl(p, s, err, err_len);
   if (rc) return rc;
   if (p->hctl->flags & PF_OVERFLOW) {
@@ -517,7 +594,9 @@ int32_t lc_part_step_end(lc_part* p, void* stream, int64_t* out_count, char* err
   }
   std::swap(p->F, p->OUTL);
   p->live &= ~p->args.bitj;
-  *out_count = (int64_t)p->hctl->ocount;
+  *out_count = (int64_t)p->hctl->oc[p->sp];
+  p->ub = p->hctl->oc[p->sp];
+  p->sp ^= 1;  // OUT becomes the frontier
   return 0;
 }
 
