@@ -363,7 +363,7 @@ def main():
         roof["note"] = ("closure tables live in LDS: HBM carries only the step streams and tile "
                         "mirrors, so the HBM fraction is small by design; the kernel's time is "
                         "the longest history's dependent chain of popcount layers (VALU issue "
-                        "and LDS latency), see DESIGN.md §3.4")
+                        "and LDS latency), see DESIGN.md §3.1")
     else:
         roof.update({"config_bytes": st["config_bytes"], "grid_phases": st["phases"],
                      "ret_steps": st["steps"], "candidates": st["candidates"],
