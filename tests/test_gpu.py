@@ -530,3 +530,35 @@ def test_gpu_partitioned_two_ranks_one_gpu_gloo():
     exp = [_oracle_part_row(h) for h in _part_cases()[3:]]
     for r in range(2):
         assert [tuple(x) for x in got[r]] == exp, (r, got[r], exp)
+
+
+# ---- offline re-check of a stored history.edn (lincheck.recheck) --------------------------
+
+def test_gpu_recheck_stored_histories(tmp_path):
+    from lincheck import recheck
+    from lincheck.history import KV
+    from test_host import ops_to_edn
+    h = synth.gen_register_keys(10, 200, 5, 0.01, config_id=1, invalid_keys=(3, 7))
+    ops = []
+    for k in range(h.n_hist):
+        for o in h.to_ops(k):
+            o["value"] = KV(h.keys[k], o["value"])
+            ops.append(o)
+    ops.sort(key=lambda o: (o["index"], o["value"].key))
+    p = tmp_path / "history.edn"
+    p.write_text(ops_to_edn(ops))
+    res = recheck.recheck(recheck.read_history(str(p), independent=True), "multi-register")
+    exp = oracle.check_many("cas-register", h, n_threads=4)
+    for k, key in enumerate(h.keys):
+        r = res["results"][key]["linear"]
+        assert r["valid?"] == {1: True, 0: False}[exp[k]["valid"]], key
+        assert r["explored"] == exp[k]["explored"], key
+    assert res["valid?"] is (all(e["valid"] == 1 for e in exp))
+    assert sorted(res["failures"]) == sorted(h.keys[k] for k in range(h.n_hist) if exp[k]["valid"] != 1)
+    # counter workload, one plain history
+    c = synth.gen_counter(300, 4, 0.0, 11)
+    pc = tmp_path / "counter.edn"
+    pc.write_text(ops_to_edn(c.to_ops(0)))
+    rc = recheck.main([str(pc), "--workload", "counter"])
+    ec = oracle.check_one("counter", c)
+    assert rc == (0 if ec["valid"] == 1 else 1)

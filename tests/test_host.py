@@ -126,3 +126,73 @@ def test_synth_shapes_follow_reference_domains():
 
 def test_seeds_follow_survey():
     assert synth.seed_for(3, 7) == 0x5EED0000 + 3007
+
+
+# ---- stored-history re-check (lincheck.edn / lincheck.recheck) ------
+
+EDN_SAMPLE = r'''
+{:type :invoke, :f :write, :value [0 3], :process 0, :time 10, :index 0}
+#jepsen.history.Op{:index 1, :time 20, :type :ok, :process 0, :f :write, :value #jepsen.independent.Tuple{:key 0, :value 3}}
+{:type :info, :f :start, :value nil, :process :nemesis, :index 2} ; a nemesis op
+#_ {:ignored true}
+{:type :invoke :f :cas :value [1 [3 4]] :process 1 :index 3 :error "x\"y" :x #{1 2} :y 1.5 :z \a}
+'''
+
+
+def _to_edn(x):
+    from lincheck.history import KV
+    if x is None:
+        return "nil"
+    if isinstance(x, KV):
+        return f"[{_to_edn(x.key)} {_to_edn(x.value)}]"
+    if isinstance(x, (list, tuple)):
+        return "[" + " ".join(_to_edn(v) for v in x) + "]"
+    if isinstance(x, str):
+        return ":" + x
+    return str(x)
+
+
+def ops_to_edn(ops):
+    return "\n".join("{" + ", ".join(f":{k} {_to_edn(v)}" for k, v in op.items()) + "}"
+                     for op in ops) + "\n"
+
+
+def test_edn_reader_sample():
+    from lincheck import edn
+    from lincheck.history import KV
+    ops = edn.read_history(EDN_SAMPLE, independent=True)
+    assert len(ops) == 4
+    assert ops[0] == {"type": "invoke", "f": "write", "value": KV(0, 3), "process": 0,
+                      "time": 10, "index": 0}
+    assert ops[1]["value"] == KV(0, 3) and ops[1]["type"] == "ok"
+    assert ops[2]["process"] == "nemesis" and ops[2]["value"] is None
+    assert ops[3]["value"] == KV(1, [3, 4]) and ops[3]["error"] == 'x"y'
+    assert ops[3]["x"] == frozenset({1, 2}) and ops[3]["y"] == 1.5 and ops[3]["z"] == "a"
+
+
+def test_edn_vector_form_and_errors():
+    from lincheck import edn
+    ops = edn.read_history("[{:type :invoke :f :read :value nil :process 0}\n"
+                           " {:type :ok :f :read :value 3 :process 0}]")
+    assert [o["type"] for o in ops] == ["invoke", "ok"] and ops[1]["value"] == 3
+    with pytest.raises(edn.EdnError):
+        list(edn.loads_all("{:a 1"))
+
+
+def test_edn_round_trip_independent_history(tmp_path):
+    from lincheck import edn, history as H, synth
+    from lincheck.history import KV
+    h = synth.gen_register_keys(4, 60, 3, 0.05, config_id=1)
+    ops = []
+    for k in range(h.n_hist):
+        for o in h.to_ops(k):
+            o["value"] = KV(h.keys[k], o["value"])
+            ops.append(o)
+    ops.sort(key=lambda o: (o["index"], o["value"].key))
+    p = tmp_path / "history.edn"
+    p.write_text(ops_to_edn(ops))
+    back = H.subhistories(edn.read_history(str(p), independent=True))
+    want = H.subhistories(ops)
+    assert back.keys == want.keys
+    for a, b in zip(back.arrays(), want.arrays()):
+        assert np.array_equal(a, b)
