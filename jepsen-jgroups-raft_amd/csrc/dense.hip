@@ -170,9 +170,8 @@ __device__ __forceinline__ uint64_t pull_hi(const uint64_t* B, const uint64_t* z
 
 // The rest of word w's closure, given R = its pulls (hi bits and other tiles): the in-word
 // closure over the 3 low bits, then the store. Returns popcount(R); *out = X | R.
-__device__ __forceinline__ uint32_t finish_word(uint64_t* B, uint32_t w, uint32_t live, int j, const OpSel* ops,
-                                               uint32_t foldm, uint64_t R, uint64_t* out) {
-  const uint64_t X = B[w];
+__device__ __forceinline__ uint64_t close_in_word(uint64_t X, uint32_t w, uint32_t live, int j, const OpSel* ops,
+                                                 uint32_t foldm, uint64_t R) {
   const bool j_lo = j < 3;
   const uint32_t jh = j_lo ? 0u : 1u << (j - 3);
   if (!(w & jh)) {
@@ -193,6 +192,13 @@ __device__ __forceinline__ uint32_t finish_word(uint64_t* B, uint32_t w, uint32_
     if (j_lo)  // the returning op, linearized last
       R |= transfer_lo(ops[j], (foldm >> j) & 1u, X | R, notj, notj64, 1 << j);
   }
+  return R;
+}
+
+__device__ __forceinline__ uint32_t finish_word(uint64_t* B, uint32_t w, uint32_t live, int j, const OpSel* ops,
+                                               uint32_t foldm, uint64_t R, uint64_t* out) {
+  const uint64_t X = B[w];
+  R = close_in_word(X, w, live, j, ops, foldm, R);
   if (R) B[w] = X | R;
   *out = X | R;
   return (uint32_t)__popcll(R);
@@ -424,6 +430,236 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
   }
 }
 
+// ---- pipelined steps (WAVE and BLOCK teams) ---------------------------------------------
+//
+// Consecutive RETURN steps of one history overlap. Step t+1's layer q reads only words of
+// popcount <= q + 1 of step t's table (its own X, through the return map below) and writes
+// words of popcount q, which step t last reads in its layer q + 1. So step t+1 may run its
+// layer q in the same super-layer as step t's layer q + 2: a step starts two super-layers
+// after its predecessor (one if the predecessor has a single layer), every running step
+// advances one layer per super-layer, and one team barrier ends each super-layer. Up to
+// (H + 1) / 2 steps are in flight; the barrier count per step falls from H + 1 to about 2.
+//
+// The return is never applied in place. Step t reads its frontier through step t-1's
+// returning slot jp: X(w) = B[w | jp] (jp a word bit), (B[w] & with_jp) >> 2^jp (jp a low
+// bit), and 0 for masks holding a slot invoked since that return ("fresh": those configs do
+// not exist yet, whatever stale words their index holds). It stores every visited word, so
+// the next step finds X | R at the word's own index. The OR of the X a step reads is step
+// t-1's post-return frontier: zero means step t-1 is the failing RETURN. An empty frontier
+// stays empty, so the steps started after a failure add no explored configs.
+constexpr int PIPE_OPN = 24;  // op-table entries per step: OP_PAD + slots 0..16, + the pull batches' tail
+struct __attribute__((aligned(16))) PipeStep {
+  OpSel ops[PIPE_OPN];  // slot k at ops[OP_PAD + k]; every entry initialised
+  uint32_t live, fresh, foldm, anyx;
+  int32_t j, jp, H, start;
+};
+
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Decode the step header at pos into dst (one whole wave): the op table is the previous
+// step's plus this step's invocations; the fresh slots are the live ones the previous step
+// did not leave pending.
+__device__ __forceinline__ void pipe_decode(const DenseParams& p, StreamWin& sw, int64_t& pos, int lane,
+                                            PipeStep* dst, const PipeStep* prev) {
+  sw.need(p, pos, lane);
+  const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sw.at(pos));
+  const int ninv = (int)(H0 >> 27);
+  const uint32_t wd = sw.at(pos + 1 + lane);
+  const uint32_t plive = prev ? (uint32_t)rfl((int)prev->live) : 0u;
+  const int pj = prev ? rfl(prev->j) : -1;
+  if (lane < PIPE_OPN) dst->ops[lane] = prev ? prev->ops[lane] : OpSel{SEL_NONE, SEL_NONE};
+  if (lane < ninv) dst->ops[OP_PAD + (wd & 31u)] = decode_op((wd >> 8) & 0xffu, (wd >> 16) & 0xffu);
+  // after the stores (one wave's LDS ops stay in order)
+  const uint32_t foldm =
+      (uint32_t)__ballot(lane < PIPE_OPN - OP_PAD && dst->ops[OP_PAD + lane].hi == OPS_FOLD);
+  if (lane == 0) {
+    const uint32_t live = H0 & 0x3fffffu;
+    const int L = 32 - __clz((int)live);
+    dst->live = live;
+    dst->fresh = prev ? live & ~(plive & ~(1u << pj)) : live;
+    dst->foldm = foldm;
+    dst->anyx = 0;
+    dst->j = (int)((H0 >> 22) & 31u);
+    dst->jp = pj;
+    dst->H = L > 3 ? L - 3 : 0;
+    dst->start = 1 << 30;  // not started
+  }
+  pos += 1 + ninv;
+}
+
+// word w's frontier before step (fresh, jp): step jp's post-return table, read in place
+__device__ __forceinline__ uint64_t pipe_x(const uint64_t* B, uint32_t w, uint32_t fresh_hi, int jp,
+                                           uint64_t keep_lo) {
+  if (w & fresh_hi) return 0;
+  uint64_t v;
+  if (jp >= 3) v = B[w | (1u << (jp - 3))];
+  else if (jp >= 0) v = (B[w] & ~keep64(jp)) >> (1 << jp);
+  else v = B[w];
+  return v & keep_lo;
+}
+
+template <typename T>
+__device__ __forceinline__ T rdl(T v, int l) {
+  return (T)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Control state is wave-uniform and identical in every wave of the team. Each super-layer
+// starts after a barrier with ONE lane-parallel read of the ring: lane i holds the header of
+// step t_ret + i. Retirement (in order, with the failure test), the running steps' layers
+// ("segments") and the next start all come from that view by ballots and readlanes.
+template <int TEAM, int TLOG, int RING>
+__device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, const uint64_t* zero,
+                                             PipeStep* ring, int* sQ, unsigned long long* sExpl,
+                                             const uint32_t* words, const uint32_t* wofs, const uint32_t* binom,
+                                             int tt, unsigned long long& st_fout, unsigned long long& st_steps) {
+  // pull batches read entries up to OP_PAD + b0 + 6 (b0 < H, a multiple of 4); slots < TLOG
+  static_assert(OP_PAD + ((TLOG - 4) / 4) * 4 + 6 < PIPE_OPN && OP_PAD + TLOG <= PIPE_OPN, "op table too small");
+  static_assert(RING <= 64, "one lane per ring entry");
+  const int lane = threadIdx.x & 63;
+  const bool decoder = tt < 64;  // the team's first wave decodes the step headers
+  for (;;) {
+    if (tt == 0) *sQ = atomicAdd(p.queue, 1);
+    team_sync<TEAM>();
+    const int qi = *sQ;
+    if (tt == 0) *sExpl = 0;
+    team_sync<TEAM>();
+    if (qi >= p.n) break;
+    const int h = p.order[qi];
+    if (p.stamps && tt == 0) p.stamps[4 * h] = __builtin_amdgcn_s_memrealtime();
+    const int lmax = p.lmax[h];
+    const int NW = lmax > 3 ? 1 << (lmax - 3) : 1;
+    const int ns = p.nsteps[h];
+    for (int i = tt; i < NW; i += TEAM) B[i] = 0;
+    team_sync<TEAM>();
+    if (tt == 0) B[0] = 1;  // (cas-register) starts at nil: state id 0, nothing linearized
+    StreamWin sw;
+    int64_t pos = p.sbeg[h];
+    if (ns > 0 && decoder) {
+      pipe_decode(p, sw, pos, lane, &ring[0], nullptr);
+      if (tt == 0) ring[0].start = 0;
+    }
+    team_sync<TEAM>();
+    unsigned long long expl = 0;
+    int fail_t = -1;
+    int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0;  // decoded, started, retired
+    for (int s = 0; t_ret < ns; ++s) {
+      // ---- ring view: lane i = step t_ret + i (decoded steps only)
+      const int tl = t_ret + lane;
+      const bool dec_l = lane < RING && tl < t_dec;
+      uint4 h0 = {0u, 0u, 0u, 0u};
+      int4 h1 = {0, 0, 0, 1 << 30};
+      if (dec_l) {
+        const PipeStep* st = &ring[tl % RING];
+        h0 = *reinterpret_cast<const uint4*>(&st->live);  // live, fresh, foldm, anyx
+        h1 = *reinterpret_cast<const int4*>(&st->j);      // j, jp, H, start
+      }
+      const bool run_l = dec_l && tl < t_run;
+      // retire the steps whose last layer ran in an earlier super-layer, in order
+      const bool fin_l = run_l && h1.w + h1.z < s;
+      const uint64_t fin = __ballot(fin_l);
+      const int lead = (int)__builtin_ctzll(~fin);
+      const uint64_t lead_mask = lead >= 64 ? ~0ull : (1ull << lead) - 1;
+      const uint64_t bad = __ballot(fin_l && tl > 0 && h0.w == 0u) & lead_mask;
+      if (bad) {  // step (first such) - 1 returned an empty frontier
+        fail_t = t_ret + (int)__builtin_ctzll(bad) - 1;
+        break;
+      }
+      const int t_ret_old = t_ret;
+      t_ret += lead;
+      if (t_ret >= ns) break;
+      // ---- segments: running steps in their layer q = s - start <= H
+      const int q_l = s - h1.w;
+      const bool seg_l = run_l && q_l >= 0 && q_l <= h1.z;
+      uint32_t nq_l = 0, o_l = 0;
+      if (seg_l) nq_l = binom[h1.z * BINOM_N + q_l], o_l = wofs[q_l];
+      uint64_t segm = __ballot(seg_l);
+      int i = segm ? (int)__builtin_ctzll(segm) : -1;
+      uint32_t wn = 0;
+      if (i >= 0 && (uint32_t)tt < rdl(nq_l, i)) wn = words[rdl(o_l, i) + tt];
+      while (i >= 0) {
+        segm &= segm - 1;
+        const int i2 = segm ? (int)__builtin_ctzll(segm) : -1;
+        uint32_t wn2 = 0;  // the next segment's first word, loaded ahead
+        if (i2 >= 0 && (uint32_t)tt < rdl(nq_l, i2)) wn2 = words[rdl(o_l, i2) + tt];
+        const uint32_t nq = rdl(nq_l, i), o = rdl(o_l, i);
+        const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i), foldm = rdl(h0.z, i);
+        const int j = rdl(h1.x, i), jp = rdl(h1.y, i), H = rdl(h1.z, i);
+        const int t = t_ret_old + i;
+        uint64_t keep_lo = ~0ull;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (fresh & (1u << k)) keep_lo &= keep64(k);
+        const uint32_t live_hi = live >> 3, fresh_hi = fresh >> 3;
+        PipeStep* st = &ring[t % RING];
+        const OpSel* ops = st->ops + OP_PAD;
+        uint64_t nzx = 0;
+        for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)TEAM) {
+          const uint32_t w = wn;
+          if (r + TEAM < nq) wn = words[o + r + TEAM];
+          if (w & ~live_hi) continue;
+          const uint64_t X = pipe_x(B, w, fresh_hi, jp, keep_lo);
+          uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+          R = close_in_word(X, w, live, j, ops, foldm, R);
+          B[w] = X | R;
+          expl += (uint32_t)__popcll(R);
+          if (t > 0) st_fout += (uint32_t)__popcll(X);
+          nzx |= X;
+        }
+        if (nzx) st->anyx = 1;
+        i = i2, wn = wn2;
+      }
+      // ---- decode ahead into a slot nobody read in this super-layer
+      const int t_dec_old = t_dec;
+      if (t_dec < ns && t_dec - t_ret_old < RING) {
+        if (decoder) pipe_decode(p, sw, pos, lane, &ring[t_dec % RING], &ring[(t_dec - 1) % RING]);
+        ++t_dec;
+      }
+      // ---- start the next decoded step at s + 1: two super-layers after its predecessor
+      // (one if that has a single layer), or at once if the predecessor retired
+      if (t_run < t_dec_old) {
+        const int lp = t_run - 1 - t_ret_old;  // the predecessor's lane (< 0: retired)
+        const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(2, rdl(h1.z, lp) + 1);
+        if (ok) {
+          if (tt == 0) ring[t_run % RING].start = s + 1;
+          ++t_run;
+        }
+      }
+      team_sync<TEAM>();
+    }
+    if (fail_t < 0 && ns > 0) {  // the last step's return
+      const PipeStep* st = &ring[(ns - 1) % RING];
+      const int jl = rfl(st->j);
+      const uint32_t live = (uint32_t)rfl((int)st->live) & ~(1u << jl);
+      const int L = live ? 32 - __clz((int)live) : 0;
+      const int nwt = 1 << (L > 3 ? L - 3 : 0);
+      uint64_t nzx = 0;
+      for (int w = tt; w < nwt; w += TEAM) {
+        if ((uint32_t)w & ~(live >> 3)) continue;
+        const uint64_t X = pipe_x(B, (uint32_t)w, 0u, jl, ~0ull);
+        st_fout += (uint32_t)__popcll(X);
+        nzx |= X;
+      }
+      if (!team_any<TEAM>(nzx != 0)) fail_t = ns - 1;
+    }
+    if (tt == 0) st_steps += fail_t >= 0 ? fail_t + 1 : ns;
+    for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
+    if constexpr (TEAM >= 256) {
+      if (lane == 0 && expl) atomicAdd(sExpl, expl);
+      __syncthreads();
+      expl = *sExpl;
+    } else {
+      expl = __shfl(expl, 0, 64);
+    }
+    if (tt == 0) {
+      p.explored[h] = expl;
+      p.fail_step[h] = fail_t;
+      p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      if (p.stamps) p.stamps[4 * h + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    team_sync<TEAM>();
+  }
+}
+
 // launch statistics (per wave, one atomic each)
 __device__ __forceinline__ void flush_stats(const DenseParams& p, unsigned long long st_fout,
                                             unsigned long long st_steps, bool step_owner) {
@@ -433,6 +669,8 @@ __device__ __forceinline__ void flush_stats(const DenseParams& p, unsigned long 
 }
 
 constexpr int WAVE_WG = 256;
+// pipeline rings: running steps <= (H + 1) / 2, plus one decoded ahead and one retire margin
+constexpr int WAVE_RING = 8, BLOCK_RING = 16;
 
 // WAVE teams: one history per wave, 4 waves per workgroup, tables of 2^DENSE_WAVE_LMAX masks.
 __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
@@ -446,6 +684,7 @@ __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
   __shared__ int sQ[NTEAM];
   __shared__ uint64_t sZero;  // the word pulls of absent bits read
   __shared__ unsigned long long sExpl[NTEAM];
+  __shared__ PipeStep sRing[NTEAM][WAVE_RING];
   const int tid = threadIdx.x, team = tid / 64, tt = tid % 64;
   init_tables(sBinom, sWOff, HMAX, WAVE_WG);
   if (tid == 0) sZero = 0;
@@ -460,8 +699,12 @@ __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
   }
   __syncthreads();
   unsigned long long st_fout = 0, st_steps = 0;
-  history_loop<64, DENSE_WAVE_LMAX>(p, &sTab[team << HMAX], &sZero, sOp[team] + OP_PAD, &sQ[team], &sExpl[team], sWords, sWOff,
-                                    sBinom, tt, st_fout, st_steps);
+  if (p.pipe & 2)
+    history_pipe<64, DENSE_WAVE_LMAX, WAVE_RING>(p, &sTab[team << HMAX], &sZero, sRing[team], &sQ[team], &sExpl[team],
+                                                 sWords, sWOff, sBinom, tt, st_fout, st_steps);
+  else
+    history_loop<64, DENSE_WAVE_LMAX>(p, &sTab[team << HMAX], &sZero, sOp[team] + OP_PAD, &sQ[team], &sExpl[team],
+                                      sWords, sWOff, sBinom, tt, st_fout, st_steps);
   flush_stats(p, st_fout, st_steps, tt == 0);
 }
 
@@ -565,6 +808,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   __shared__ unsigned sAny;
   __shared__ unsigned long long sRed;
   __shared__ uint64_t sZero;
+  __shared__ PipeStep sRing[BLOCK_RING];
 
   const int tid = threadIdx.x, lane = tid & 63;
   init_tables(sBinom, sWOff, DENSE_WORD_BITS, 1024);
@@ -574,7 +818,12 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   unsigned long long st_fout = 0, st_steps = 0;
 
   if ((int)blockIdx.x >= p.n_team_wgs) {  // ------------------------------- BLOCK histories
-    history_loop<1024, DENSE_LMAX>(p, sTab, &sZero, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout, st_steps);
+    if (p.pipe & 1)
+      history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
+                                                 st_fout, st_steps);
+    else
+      history_loop<1024, DENSE_LMAX>(p, sTab, &sZero, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout,
+                                     st_steps);
     flush_stats(p, st_fout, st_steps, tid == 0);
     return;
   }

@@ -55,6 +55,9 @@ struct DenseParams {
   int32_t* abort;               // set when a team barrier / token wait times out
   unsigned long long* tstamps;  // [n_team_wgs][8] LC_DEBUG phase cycles of each tile workgroup
   unsigned long long* lhist;    // LC_DEBUG [2 teams (wave, block)][32 widths][LH_N]; may be null
+                                // (per-step loop only)
+  int32_t pipe;                 // bit 0: BLOCK, bit 1: WAVE teams overlap consecutive steps
+                                // (history_pipe); default BLOCK only
 };
 
 // Kernels: WAVE = 256-thread workgroups, one history per wave (width <= DENSE_WAVE_LMAX);

@@ -136,6 +136,7 @@ struct lc_plan {
   int dgrid_b = 0, dgrid_w = 0;
   int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
   int tile_lbits = DENSE_LMAX;                        // LC_TILE_LBITS: local slots per tile
+  int dense_pipe = 1;  // LC_PIPE: bit 0 BLOCK, bit 1 WAVE teams overlap steps (0: one step at a time)
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_w0 = nullptr, ev_w1 = nullptr;  // per dense kernel
@@ -227,6 +228,7 @@ struct lc_plan {
     if ((e = getenv("LC_TILE_WGS")) && atoi(e) > 0) tile_cap = atoi(e);
     if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
+    if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e);
     // test hooks: shrink the keys kernel's per-workgroup capacities to force the fallback
     if ((e = getenv("LC_KCAP")) && atoll(e) > 0) kfcap = klcap = atoll(e);
     // test hooks: tiny cells / overflow buckets exercise the overflow and regrow paths
@@ -388,6 +390,7 @@ struct lc_plan {
     p.explored = d_dexpl.as<unsigned long long>();
     p.stats = d_stats.as<unsigned long long>();
     p.stamps = nullptr;
+    p.pipe = dense_pipe;
     if (debug()) {
       HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
       HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));

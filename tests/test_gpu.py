@@ -332,6 +332,29 @@ def test_gpu_dense_tables_vs_oracle():
     p.close()
 
 
+@pytest.mark.parametrize("pipe", ["0", "1", "2", "3"])
+def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
+    """LC_PIPE bit 0 / bit 1: BLOCK / WAVE teams overlap consecutive RETURN steps (step t+1's
+    layer q beside step t's layer q + 2, returns read through the previous step's slot, fresh
+    slots masked). Every mode is bit-exact with the oracle, invalid histories included (the
+    failing step is found from the next step's empty frontier)."""
+    monkeypatch.setenv("LC_PIPE", pipe)
+    hs = [synth.gen_register_keys(24, 600, 5, 0.01, config_id=3, invalid_keys=(1, 7, 16))]
+    hs += [synth.gen_register(120, 5, 0.1, 33000 + t, invalid=(t % 2 == 1)) for t in range(8)]
+    hs += [synth.gen_register(40, 3, 0.0, 34000 + t, invalid=(t % 3 == 0)) for t in range(6)]
+    h = H.concat(hs)
+    widths = [_live_width(h, k) for k in range(h.n_hist)]
+    assert min(widths) <= 11 and any(12 <= w <= 17 for w in widths)
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    g = p.results()
+    exp = oracle.check_many("cas-register", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"pipe={pipe} w={widths[k]}")
+    assert any(e["valid"] == 0 for e in exp)
+    p.close()
+
+
 _WIDE = {}
 
 
