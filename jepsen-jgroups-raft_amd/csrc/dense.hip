@@ -451,7 +451,8 @@ constexpr int PIPE_OPN = 24;  // op-table entries per step: OP_PAD + slots 0..16
 struct __attribute__((aligned(16))) PipeStep {
   OpSel ops[PIPE_OPN];  // slot k at ops[OP_PAD + k]; every entry initialised
   uint32_t live, fresh, foldm, anyx;
-  int32_t j, jp, H, start;
+  int32_t j, jp, H, start;  // H: layers - 1 over the LOCAL slots (all slots outside tile teams)
+  int32_t pstart, hp, pad0, pad1;  // tile teams: the previous step's start and H
 };
 
 __device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -460,7 +461,7 @@ __device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlan
 // step's plus this step's invocations; the fresh slots are the live ones the previous step
 // did not leave pending.
 __device__ __forceinline__ void pipe_decode(const DenseParams& p, StreamWin& sw, int64_t& pos, int lane,
-                                            PipeStep* dst, const PipeStep* prev) {
+                                            PipeStep* dst, const PipeStep* prev, uint32_t lmask = ~0u) {
   sw.need(p, pos, lane);
   const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sw.at(pos));
   const int ninv = (int)(H0 >> 27);
@@ -473,8 +474,8 @@ __device__ __forceinline__ void pipe_decode(const DenseParams& p, StreamWin& sw,
   const uint32_t foldm =
       (uint32_t)__ballot(lane < PIPE_OPN - OP_PAD && dst->ops[OP_PAD + lane].hi == OPS_FOLD);
   if (lane == 0) {
-    const uint32_t live = H0 & 0x3fffffu;
-    const int L = 32 - __clz((int)live);
+    const uint32_t live = H0 & 0x3fffffu, lloc = live & lmask;
+    const int L = lloc ? 32 - __clz((int)lloc) : 0;
     dst->live = live;
     dst->fresh = prev ? live & ~(plive & ~(1u << pj)) : live;
     dst->foldm = foldm;
@@ -483,6 +484,7 @@ __device__ __forceinline__ void pipe_decode(const DenseParams& p, StreamWin& sw,
     dst->jp = pj;
     dst->H = L > 3 ? L - 3 : 0;
     dst->start = 1 << 30;  // not started
+    dst->hp = prev ? prev->H : 0;
   }
   pos += 1 + ninv;
 }
@@ -783,6 +785,288 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
   return r;
 }
 
+// ---- pipelined tile team (DenseParams.pipe bit 2) ----------------------------------------
+//
+// Every tile walks the step stream itself and runs the pipelined schedule of history_pipe
+// (layers over its LOCAL slots, identical on every tile, so all tiles agree on every
+// super-layer's segments). A step whose live slots include team slots is "wide": its
+// words are published to the tile's mirror slot for that step (MRING slots per tile, in
+// word-list order) and successors pull them. Per super-layer a tile waits, before any work,
+// until (1) every predecessor it pulls from (tile r \ b, or r \ j for a tile holding the
+// returning j) has finished the same super-layer, and (2) for a step whose previous step
+// returned a team slot jp, tile r | jp (which holds that step's post-return frontier for
+// r's masks) has finished the previous step's same layer, i.e. super-layer pstart + q.
+// Then it works, drains its sc1 mirror stores, and stores its token = super-layers done.
+// Dependencies (1) point to tiles with fewer team bits and (2) to the previous step two
+// super-layers back, so the team runs as a skewed pipeline. Every 8 super-layers each tile
+// waits until all tokens are within 8 super-layers of its own, so a mirror slot is reused
+// only after all its readers passed it (MRING = 32 > 16 + the widest step's 15 layers).
+// Failures are decided after the last step: each tile ORs "read a nonzero X in step t"
+// into the team's bit t in HBM; the leader's first missing bit t names step t - 1.
+constexpr int MRING = DENSE_MRING;
+
+__device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
+                                           unsigned long long need, uint64_t t0, long& spins) {
+  if (ld_agent(f) >= need) return true;
+  __builtin_amdgcn_s_sleep(1);
+  if ((++spins & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull || ld_agent(p.abort))) {
+    st_agent(p.abort, 1);
+    return true;  // gives up: the caller sees the abort flag
+  }
+  return false;
+}
+
+__device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, const uint64_t* zero, PipeStep* ring,
+                                          const uint32_t* cum, const uint32_t* binom, const uint32_t* wofs,
+                                          int team, int base, int rank, int G, int h, int lb, int* sAbort,
+                                          unsigned long long& expl, unsigned long long& st_fout) {
+  constexpr int HSOLO = DENSE_LMAX - 3;
+  constexpr int RING = 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool decoder = tid < 64;
+  const uint32_t lmask = (1u << lb) - 1;
+  unsigned long long* const flags = p.flags + base;
+  uint32_t* const anyv = p.team_any + p.team_any_off[team];
+  auto mirror = [&](int r, int t) {
+    return p.mirror + (((size_t)(base + r) * MRING + (size_t)(t % MRING)) << HSOLO);
+  };
+  const int ns = p.nsteps[h];
+  // LC_DEBUG phase cycles: pred/X waits, segments, publish + token, credit waits, -, super-layers
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+  auto now = []() { return __builtin_amdgcn_s_memrealtime(); };
+  const bool timed = p.tstamps != nullptr;
+  if (p.stamps && rank == 0 && tid == 0) p.stamps[4 * h] = now();
+  if (rank == 0 && tid == 0) B[0] = 1;  // (cas-register) starts at nil: state id 0
+  StreamWin sw;
+  int64_t pos = p.sbeg[h];
+  if (ns > 0 && decoder) {
+    pipe_decode(p, sw, pos, lane, &ring[0], nullptr, lmask);
+    if (tid == 0) ring[0].start = 0, ring[0].pstart = 0;
+  }
+  __syncthreads();
+  int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0, last_start = 0;
+  for (int s = 0; t_ret < ns; ++s) {
+    unsigned long long tp = timed ? now() : 0;
+    if (s >= 8 && (s & 7) == 0) {  // credit: nobody more than 8 super-layers behind
+      if (decoder) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        long spins = 0;
+        while (!__all(lane >= G || poll_until(p, &flags[lane < G ? lane : 0], (unsigned long long)(s - 8), t0, spins)))
+          ;
+        if (tid == 0) *sAbort = ld_agent(p.abort);
+      }
+      __syncthreads();
+      if (*sAbort) break;
+      if (timed) ph[3] += now() - tp, tp = now();
+    }
+    // ---- ring view: lane i = step t_ret + i
+    const int tl = t_ret + lane;
+    const bool dec_l = lane < RING && tl < t_dec;
+    uint4 h0 = {0u, 0u, 0u, 0u};
+    int4 h1 = {0, 0, 0, 1 << 30}, h2 = {0, 0, 0, 0};
+    if (dec_l) {
+      const PipeStep* st = &ring[tl % RING];
+      h0 = *reinterpret_cast<const uint4*>(&st->live);  // live, fresh, foldm, anyx
+      h1 = *reinterpret_cast<const int4*>(&st->j);      // j, jp, H, start
+      h2 = *reinterpret_cast<const int4*>(&st->pstart); // pstart, hp
+    }
+    const bool run_l = dec_l && tl < t_run;
+    const bool fin_l = run_l && h1.w + h1.z < s;
+    const uint64_t fin = __ballot(fin_l);
+    const int lead = (int)__builtin_ctzll(~fin);
+    // retired steps: this tile read a nonzero frontier in step tl => step tl - 1 survived here
+    if (decoder && lane < lead && tl > 0 && h0.w)
+      __hip_atomic_fetch_or(&anyv[tl >> 5], 1u << (tl & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int t_ret_old = t_ret;
+    t_ret += lead;
+    if (t_ret >= ns) break;
+    // ---- segments of this tile: running steps whose team slots cover the tile
+    const uint32_t lteam_l = h0.x >> lb;
+    const int q_l = s - h1.w;
+    const bool seg_l = run_l && (rank & ~lteam_l) == 0 && q_l >= 0 && q_l <= h1.z;
+    uint32_t nq_l = 0, o_l = 0, mo_l = 0, mp_l = 0;
+    uint32_t pm_l = 0;  // team bits b: pull from tile rank ^ b at this super-layer
+    int xs_l = -1;      // tile holding this step's X (previous step returned a team slot)
+    if (seg_l) {
+      nq_l = binom[h1.z * BINOM_N + q_l], o_l = wofs[q_l], mo_l = cum[h1.z * BINOM_N + q_l];
+      mp_l = cum[h2.y * BINOM_N + min(q_l, h2.y)];
+      const int jt = h1.x >= lb ? h1.x - lb : -1;
+      const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
+      pm_l = lteam_l == 0 ? 0u : tile_j ? (1u << jt) : ((uint32_t)rank & lteam_l);
+      if (h1.y >= lb && !((uint32_t)rank & (h0.y >> lb))) xs_l = rank | (1 << (h1.y - lb));
+    }
+    if (__any(pm_l != 0 || xs_l >= 0)) {  // wait for the tiles this super-layer reads
+      if (decoder) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        long spins = 0;
+        for (;;) {
+          bool ok = true;
+          for (uint32_t m = pm_l; m && ok; m &= m - 1)
+            ok = poll_until(p, &flags[rank ^ (1 << __builtin_ctz(m))], (unsigned long long)(s + 1), t0, spins);
+          if (ok && xs_l >= 0) ok = poll_until(p, &flags[xs_l], (unsigned long long)(h2.x + q_l + 1), t0, spins);
+          if (__all(ok)) break;
+        }
+      }
+      __syncthreads();
+      if (timed) ph[0] += now() - tp, tp = now();
+    }
+    uint64_t segm = __ballot(seg_l);
+    const bool wide_any = __ballot(seg_l && lteam_l != 0) != 0;
+    // TW words per thread at a time, each chunk's word indices loaded one chunk ahead (the
+    // next segment's first chunk while this segment runs)
+    constexpr int TW = 2, TB = DENSE_WIDE_LMAX - DENSE_LMAX;
+    int i = segm ? (int)__builtin_ctzll(segm) : -1;
+    uint32_t wn[TW];
+#pragma unroll
+    for (int k = 0; k < TW; ++k) {
+      const uint32_t r = (uint32_t)tid + 1024u * k;
+      wn[k] = (i >= 0 && r < rdl(nq_l, i)) ? p.words[rdl(o_l, i) + r] : ~0u;
+    }
+    while (i >= 0) {
+      segm &= segm - 1;
+      const int i2 = segm ? (int)__builtin_ctzll(segm) : -1;
+      uint32_t wn2[TW];
+#pragma unroll
+      for (int k = 0; k < TW; ++k) {
+        const uint32_t r = (uint32_t)tid + 1024u * k;
+        wn2[k] = (i2 >= 0 && r < rdl(nq_l, i2)) ? p.words[rdl(o_l, i2) + r] : ~0u;
+      }
+      const uint32_t nq = rdl(nq_l, i), mo = rdl(mo_l, i), mp = rdl(mp_l, i), pmask = rdl(pm_l, i);
+      const uint32_t o = rdl(o_l, i);
+      const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i), foldm = rdl(h0.z, i);
+      const int j = rdl(h1.x, i), jp = rdl(h1.y, i), H = rdl(h1.z, i), xs = rdl(xs_l, i);
+      const int t = t_ret_old + i;
+      const uint32_t live_loc = live & lmask, lteam = live >> lb;
+      const bool wide = lteam != 0;
+      const int jt = j >= lb ? j - lb : -1;
+      const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
+      const bool jloc_hi = j >= 3 && j < lb;
+      const bool tile_fresh = ((uint32_t)rank & (fresh >> lb)) != 0;  // the tile's masks start empty
+      uint64_t keep_lo = ~0ull;
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (fresh & (1u << k)) keep_lo &= keep64(k);
+      const uint32_t live_hi = live_loc >> 3, fresh_hi = (fresh & lmask) >> 3;
+      PipeStep* st = &ring[t % RING];
+      const OpSel* ops = st->ops + OP_PAD;
+      const uint64_t* xsrc = xs >= 0 ? mirror(xs, t - 1) + mp : nullptr;
+      uint64_t* mine = mirror(rank, t) + mo;
+      uint64_t nzx = 0;
+      if (!wide && !xsrc) {  // a step on this tile alone: the BLOCK loop (LDS only)
+        for (uint32_t r0 = (uint32_t)tid; r0 < nq; r0 += 1024u * TW) {
+#pragma unroll
+          for (int k = 0; k < TW; ++k) {
+            const uint32_t r = r0 + 1024u * k, rn = r + 1024u * TW;
+            const uint32_t w = wn[k];
+            wn[k] = rn < nq ? p.words[o + rn] : ~0u;
+            if (r >= nq || (w & ~live_hi)) continue;
+            const uint64_t X = tile_fresh ? 0ull : pipe_x(B, w, fresh_hi, jp, keep_lo);
+            uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+            R = close_in_word(X, w, live_loc, j, ops, foldm, R);
+            B[w] = X | R;
+            expl += (uint32_t)__popcll(R);
+            if (t > 0) st_fout += (uint32_t)__popcll(X);
+            nzx |= X;
+          }
+        }
+      } else
+      // every HBM load of a chunk (X from tile xs, one pull per predecessor tile) is issued
+      // before any is used
+      for (uint32_t r0 = (uint32_t)tid; r0 < nq; r0 += 1024u * TW) {
+        uint32_t wl[TW];
+        bool ok[TW];
+        uint64_t xv[TW], pv[TW][TB];
+#pragma unroll
+        for (int k = 0; k < TW; ++k) {
+          const uint32_t r = r0 + 1024u * k, rn = r + 1024u * TW;
+          wl[k] = wn[k];
+          wn[k] = rn < nq ? p.words[o + rn] : ~0u;
+          ok[k] = r < nq && !(wl[k] & ~live_hi);
+        }
+#pragma unroll
+        for (int k = 0; k < TW; ++k) {
+          const uint32_t r = r0 + 1024u * k;
+          const bool fx = ok[k] && !tile_fresh && !(wl[k] & fresh_hi);
+          xv[k] = (fx && xsrc) ? HbmTab::ld(xsrc + r) : 0ull;
+          // pulls from the tiles one team bit below: none for masks holding a local j (never
+          // expanded); a tile holding j takes only T_j of r \ j
+          const bool pl = ok[k] && (tile_j || !(jloc_hi && ((wl[k] >> (j - 3)) & 1u)));
+#pragma unroll
+          for (int b = 0; b < TB; ++b)
+            pv[k][b] = (pl && ((pmask >> b) & 1u)) ? HbmTab::ld(mirror(rank ^ (1 << b), t) + mo + r) : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < TW; ++k) {
+          if (!ok[k]) continue;
+          const uint32_t w = wl[k], r = r0 + 1024u * k;
+          uint64_t X = xv[k] & keep_lo;
+          if (!xsrc && !tile_fresh && !(w & fresh_hi) && jp < lb) X = pipe_x(B, w, 0u, jp, keep_lo);
+          uint64_t R = tile_j ? 0ull : pull_hi<4>(B, zero, w, j, H, ops, foldm);
+#pragma unroll
+          for (int b = 0; b < TB; ++b)
+            if ((pmask >> b) & 1u) R |= transfer(ops[lb + b], (foldm >> (lb + b)) & 1u, pv[k][b]);
+          if (!tile_j) R = close_in_word(X, w, live_loc, j, ops, foldm, R);
+          const uint64_t nv = X | R;
+          B[w] = nv;
+          if (wide) HbmTab::st(mine + r, nv);
+          expl += (uint32_t)__popcll(R);
+          if (t > 0) st_fout += (uint32_t)__popcll(X);
+          nzx |= X;
+        }
+      }
+      if (nzx) st->anyx = 1;
+      i = i2;
+#pragma unroll
+      for (int k = 0; k < TW; ++k) wn[k] = wn2[k];
+    }
+    const int t_dec_old = t_dec;
+    if (t_dec < ns && t_dec - t_ret_old < RING) {
+      if (decoder) pipe_decode(p, sw, pos, lane, &ring[t_dec % RING], &ring[(t_dec - 1) % RING], lmask);
+      ++t_dec;
+    }
+    if (t_run < t_dec_old) {
+      const int lp = t_run - 1 - t_ret_old;
+      const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(2, rdl(h1.z, lp) + 1);
+      if (ok) {
+        if (tid == 0) ring[t_run % RING].start = s + 1, ring[t_run % RING].pstart = last_start;
+        last_start = s + 1;
+        ++t_run;
+      }
+    }
+    if (timed) ph[1] += now() - tp, tp = now();
+    if (wide_any) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+    if (tid == 0) st_agent(&flags[rank], (unsigned long long)(s + 1));
+    if (timed) ph[2] += now() - tp, ph[5] += 1;
+  }
+  if (timed && tid == 0)
+    for (int k = 0; k < 6; ++k) p.tstamps[blockIdx.x * 8 + k] = ph[k];
+  // make sure the last token is out before the team barrier's readers look (the barrier orders it)
+  if (ns > 0) {  // the last step's return, over this tile, once every tile has finished
+    team_bar((TeamCtl*)p.ctl + team, G, p.abort, sAbort);
+    const PipeStep* st = &ring[(ns - 1) % RING];
+    const int jl = rfl(st->j), H = rfl(st->H);
+    const uint32_t live = (uint32_t)rfl((int)st->live) & ~(1u << jl);
+    const uint32_t live_hi = (live & lmask) >> 3;
+    uint64_t nzx = 0;
+    if (((uint32_t)rank & ~(live >> lb)) == 0) {
+      const uint64_t* xsrc = jl >= lb ? mirror(rank | (1 << (jl - lb)), ns - 1) : nullptr;
+      for (int q = 0; q <= H; ++q) {
+        const uint32_t nq = binom[H * BINOM_N + q], o = wofs[q], mo = cum[H * BINOM_N + q];
+        for (uint32_t r = (uint32_t)tid; r < nq; r += 1024u) {
+          const uint32_t w = p.words[o + r];
+          if (w & ~live_hi) continue;
+          const uint64_t X = xsrc ? HbmTab::ld(xsrc + mo + r) : pipe_x(B, w, 0u, jl, ~0ull);
+          st_fout += (uint32_t)__popcll(X);
+          nzx |= X;
+        }
+      }
+    }
+    if (__syncthreads_or(nzx != 0) && tid == 0)
+      __hip_atomic_fetch_or(&anyv[ns >> 5], 1u << (ns & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // BLOCK histories and TILE teams in one launch (same 1024-thread, 128 KiB-LDS workgroups, so
 // every workgroup is resident: the grid never exceeds one workgroup per CU).
 //
@@ -809,9 +1093,15 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   __shared__ unsigned long long sRed;
   __shared__ uint64_t sZero;
   __shared__ PipeStep sRing[BLOCK_RING];
+  __shared__ uint32_t sCum[BINOM_N * BINOM_N];  // sCum[n][k] = sum of C(n, q) for q < k
 
   const int tid = threadIdx.x, lane = tid & 63;
   init_tables(sBinom, sWOff, DENSE_WORD_BITS, 1024);
+  for (int i = tid; i < BINOM_N * BINOM_N; i += 1024) {
+    uint32_t c = 0;
+    for (int q = 0; q < i % BINOM_N; ++q) c += sBinom[(i / BINOM_N) * BINOM_N + q];
+    sCum[i] = c;
+  }
   if (tid == 0) sAbort = 0, sZero = 0;
   if (tid < OP_TAB) sOpT[tid] = OpSel{SEL_NONE, SEL_NONE};  // (see dense_wave_kernel)
   __syncthreads();
@@ -847,6 +1137,26 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   for (int i = tid; i < (1 << HSOLO); i += 1024) sTab[i] = 0;
   __syncthreads();
   if (rank == 0 && tid == 0) sTab[0] = 1;  // (cas-register) starts at nil: state id 0
+
+  if (p.pipe & 4) {  // pipelined tile team
+    team_pipe(p, sTab, &sZero, sRing, sCum, sBinom, sWOff, team, base, rank, G, h, lb, &sAbort, expl, st_fout);
+    bar();  // every tile's survivor bits are in
+    if (rank == 0 && tid == 0) {
+      const int ns = p.nsteps[h];
+      const uint32_t* anyv = p.team_any + p.team_any_off[team];
+      int fail_t = -1;
+      for (int t = 1; t <= ns && fail_t < 0; ++t)
+        if (!((ld_agent(&anyv[t >> 5]) >> (t & 31)) & 1u)) fail_t = t - 1;
+      p.fail_step[h] = fail_t;
+      p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      st_steps += fail_t >= 0 ? fail_t + 1 : ns;
+      if (p.stamps) p.stamps[4 * h + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    const unsigned long long e = block_sum(expl, &sRed);
+    if (tid == 0 && e) atomicAdd(&p.explored[h], e);
+    flush_stats(p, st_fout, st_steps, tid == 0);
+    return;
+  }
 
   // one step of width > 17 on every tile (the ops are in sOp); returns "survived"
   auto team_step = [&](long long hpos) -> bool {

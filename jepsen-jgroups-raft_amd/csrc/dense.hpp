@@ -19,6 +19,7 @@ constexpr int DENSE_WAVE_LMAX = 11;  // histories this narrow run one per wave
 constexpr int DENSE_WIDE_LMAX = 22;  // widest table a tile team holds (2^(22-17) LDS tiles)
 constexpr int DENSE_MAX_STATES = 8;  // register values (state ids) per history
 constexpr int DENSE_WORD_BITS = DENSE_WIDE_LMAX - 3;  // bits of the sorted word list
+constexpr int DENSE_MRING = 32;      // mirror slots per tile (pipelined tile teams)
 
 // Step stream (host-built, one u32 word stream per history):
 //   header  live[0:22) | j[22:27) | ninv[27:32)   live = pending slots after this step's
@@ -49,15 +50,18 @@ struct DenseParams {
   const int8_t* team_bits;      // [teams] t: 2^t workgroups, history width <= lb + t
   const int8_t* team_lbits;     // [teams] lb: local slots per tile (<= DENSE_LMAX)
   const int32_t* team_hist;     // [teams] history id
-  uint64_t* mirror;             // [n_team_wgs][2^(DENSE_LMAX-3)] published tile words
+  uint64_t* mirror;             // [n_team_wgs][DENSE_MRING][2^(DENSE_LMAX-3)] published tile words
+                                // (one slot per step in flight when pipelined, else slot 0)
   unsigned long long* flags;    // [n_team_wgs] layer tokens (zeroed before launch)
   void* ctl;                    // [teams] TeamCtl (zeroed before launch)
   int32_t* abort;               // set when a team barrier / token wait times out
   unsigned long long* tstamps;  // [n_team_wgs][8] LC_DEBUG phase cycles of each tile workgroup
   unsigned long long* lhist;    // LC_DEBUG [2 teams (wave, block)][32 widths][LH_N]; may be null
                                 // (per-step loop only)
-  int32_t pipe;                 // bit 0: BLOCK, bit 1: WAVE teams overlap consecutive steps
-                                // (history_pipe); default BLOCK only
+  uint32_t* team_any;           // pipelined teams: per team, bit t = some tile read a nonzero
+  const int32_t* team_any_off;  // frontier in step t (step ns: the last return); word offsets
+  int32_t pipe;                 // bit 0: BLOCK, bit 1: WAVE, bit 2: TILE teams overlap
+                                // consecutive steps (history_pipe / team_pipe)
 };
 
 // Kernels: WAVE = 256-thread workgroups, one history per wave (width <= DENSE_WAVE_LMAX);

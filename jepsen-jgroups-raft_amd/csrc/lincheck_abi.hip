@@ -128,6 +128,7 @@ struct lc_plan {
   // dense closure tables (narrow cas-register histories; dense.hpp)
   std::vector<int> dense_b, dense_w, dense_x;  // block / wave / wide teams, heaviest first
   DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dwords, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
+  DevArray d_tany, d_tanyoff;
   DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_tlbits, d_thist;
   struct StepBytes { double lds, hbm; };
   std::vector<StepBytes> dalg;     // per dense step: algorithmic bytes
@@ -444,8 +445,29 @@ struct lc_plan {
       max_wgs = std::max(max_wgs, l_wgteam[l].size());
       max_teams = std::max(max_teams, l_base[l].size());
     }
+    // pipelined teams: per team one survivor bit per step (+ the last return), in u32 words
+    std::vector<std::vector<int32_t>> l_anyoff(launches.size());
+    size_t max_anyw = 0;
+    for (size_t l = 0; l < launches.size(); ++l) {
+      int32_t o = 0;
+      for (int h : launches[l]) {
+        l_anyoff[l].push_back(o);
+        o += enc.n_steps(h) / 32 + 1;
+      }
+      max_anyw = std::max(max_anyw, (size_t)o);
+    }
+    // pipelined teams pull over at most DENSE_WIDE_LMAX - DENSE_LMAX team bits per tile
+    // (LC_TILE_LBITS below 17 can make more): such launches use the per-step team loop
+    int pipe_mode = dense_pipe;
+    for (size_t l = 0; l < launches.size(); ++l)
+      for (int8_t t : l_bits[l])
+        if (t > DENSE_WIDE_LMAX - DENSE_LMAX) pipe_mode &= ~4;
+    p.pipe = pipe_mode;
     if (max_wgs) {
-      HIP_TRY(d_mirror.ensure((max_wgs << (DENSE_LMAX - 3)) * 8));
+      const size_t slots = (pipe_mode & 4) ? DENSE_MRING : 1;
+      HIP_TRY(d_mirror.ensure((max_wgs * slots << (DENSE_LMAX - 3)) * 8));
+      HIP_TRY(d_tany.ensure(std::max<size_t>(max_anyw, 1) * 4));
+      HIP_TRY(d_tanyoff.ensure(max_teams * 4));
       HIP_TRY(d_tflags.ensure(max_wgs * 8));
       HIP_TRY(d_ctl.ensure(max_teams * dense_ctl_bytes()));
       HIP_TRY(d_abort.ensure(16));
@@ -485,6 +507,10 @@ struct lc_plan {
         HIP_TRY(hipMemcpyAsync(d_thist.p, l_hist[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemsetAsync(d_tflags.p, 0, (size_t)twgs * 8, stream));
         HIP_TRY(hipMemsetAsync(d_ctl.p, 0, (size_t)nt * dense_ctl_bytes(), stream));
+        HIP_TRY(hipMemcpyAsync(d_tanyoff.p, l_anyoff[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemsetAsync(d_tany.p, 0, std::max<size_t>(max_anyw, 1) * 4, stream));
+        q.team_any = d_tany.as<uint32_t>();
+        q.team_any_off = d_tanyoff.as<int32_t>();
         q.wg_team = d_wgteam.as<int32_t>();
         q.team_base = d_tbase.as<int32_t>();
         q.team_bits = d_tbits.as<int8_t>();
@@ -569,8 +595,9 @@ struct lc_plan {
         if (hipMemcpy(TS.data(), d_tstamps.p, TS.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
           for (int r = 0; r < g0; ++r) {
             const double st = std::max(1.0, (double)TS[r * 8 + 5]);
-            fprintf(stderr, "[lincheck]     tile team h=%d rank %2d: per team step us: wait %.1f compute %.1f "
-                    "publish %.1f return %.1f barrier %.1f (%.0f steps)\n", l_hist[0][0], r, TS[r * 8] / st / 100,
+            fprintf(stderr, (p.pipe & 4) ? "[lincheck]     tile team h=%d rank %2d: per super-layer us: wait %.2f "
+                    "compute %.2f publish %.2f credit %.2f - %.2f (%.0f super-layers)\n" : "[lincheck]     tile team "
+                    "h=%d rank %2d: per team step us: wait %.1f compute %.1f publish %.1f return %.1f barrier %.1f (%.0f steps)\n", l_hist[0][0], r, TS[r * 8] / st / 100,
                     TS[r * 8 + 1] / st / 100, TS[r * 8 + 2] / st / 100, TS[r * 8 + 3] / st / 100,
                     TS[r * 8 + 4] / st / 100, st);
           }

@@ -398,6 +398,24 @@ def test_gpu_dense_tile_teams(cap, monkeypatch):
     p.close()
 
 
+@pytest.mark.parametrize("lbits", [None, "15"])
+def test_gpu_dense_tile_teams_pipelined(lbits, monkeypatch):
+    """LC_PIPE bit 2: tile teams overlap steps (team_pipe: per-step mirror slots, super-layer
+    tokens, X of a team-slot return read from tile r | j, survivors as per-step bits in HBM).
+    With 15-bit tiles a team has more team bits than the pipelined pulls cover, and the
+    launch must fall back to the per-step team loop: same answers either way."""
+    monkeypatch.setenv("LC_PIPE", "5")
+    if lbits:
+        monkeypatch.setenv("LC_TILE_LBITS", lbits)
+    h, widths, exp = _wide_batch()
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    got = p.results()
+    for k in range(h.n_hist):
+        _cmp(got, exp[k], k, f"pipelined tile lbits={lbits} w={widths[k]}")
+    p.close()
+
+
 def test_gpu_dense_width_limit_routes_to_grid(monkeypatch):
     """LC_DENSE_MAXW=17 sends the wide histories to the sparse grid kernel: same answers."""
     h, widths, exp = _wide_batch()
