@@ -137,6 +137,7 @@ struct lc_plan {
   int dgrid_b = 0, dgrid_w = 0;
   int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
   int tile_lbits = DENSE_LMAX;                        // LC_TILE_LBITS: local slots per tile
+  int wide_from = 99, wide_lbits = DENSE_LMAX;        // LC_TILE_WIDE=w:b: b local slots from width w
   int dense_pipe = 1;  // LC_PIPE: bit 0 BLOCK, bit 1 WAVE teams overlap steps (0: one step at a time)
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -230,6 +231,10 @@ struct lc_plan {
     if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e);
+    if ((e = getenv("LC_TILE_WIDE")) && strchr(e, ':')) {
+      wide_from = atoi(e);
+      wide_lbits = std::max(12, std::min(atoi(strchr(e, ':') + 1), DENSE_LMAX));
+    }
     // test hooks: shrink the keys kernel's per-workgroup capacities to force the fallback
     if ((e = getenv("LC_KCAP")) && atoll(e) > 0) kfcap = klcap = atoll(e);
     // test hooks: tiny cells / overflow buckets exercise the overflow and regrow paths
@@ -411,7 +416,8 @@ struct lc_plan {
     while ((2 << grid_log) <= dgrid_b) ++grid_log;
     auto lbits_of = [&](int h) {
       const int lw = enc.live_max[h];
-      return std::min(DENSE_LMAX, std::max(lw - grid_log, std::min(tile_lbits, lw - 1)));
+      const int want = lw >= wide_from ? std::min(wide_lbits, tile_lbits) : tile_lbits;
+      return std::min(DENSE_LMAX, std::max(lw - grid_log, std::min(want, lw - 1)));
     };
     for (int h : dense_x) {
       const int g = 1 << (enc.live_max[h] - lbits_of(h));
