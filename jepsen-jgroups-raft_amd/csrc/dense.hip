@@ -575,6 +575,50 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       uint32_t nq_l = 0, o_l = 0;
       if (seg_l) nq_l = binom[h1.z * BINOM_N + q_l], o_l = wofs[q_l];
       uint64_t segm = __ballot(seg_l);
+      if constexpr (TEAM == 64) {
+        // one wave: the segments' words are packed over the lanes (flat index f -> segment i,
+        // rank r), every lane with its own step's parameters, so a super-layer of several
+        // small layers is one pass instead of one pass per segment
+        uint32_t inc = nq_l;  // inclusive prefix of the word counts over the ring lanes
+#pragma unroll
+        for (int d = 1; d < RING; d <<= 1) {
+          const uint32_t v = (uint32_t)__shfl_up((int)inc, d, 64);
+          if (lane >= d) inc += v;
+        }
+        const uint32_t exc = inc - nq_l, total = rdl(inc, RING - 1);
+        // passes are wave-uniform: a shuffle reads 0 from an inactive source lane
+        for (uint32_t f0 = 0; f0 < total; f0 += 64u) {
+          const uint32_t f = f0 + (uint32_t)lane;
+          int i = 0;
+          for (uint64_t m = segm; m; m &= m - 1) {
+            const int k = (int)__builtin_ctzll(m);
+            if (f >= rdl(exc, k)) i = k;
+          }
+          const uint32_t r = f - (uint32_t)__shfl((int)exc, i, 64);
+          const uint32_t o = (uint32_t)__shfl((int)o_l, i, 64);
+          const uint32_t live = (uint32_t)__shfl((int)h0.x, i, 64), fresh = (uint32_t)__shfl((int)h0.y, i, 64);
+          const uint32_t foldm = (uint32_t)__shfl((int)h0.z, i, 64);
+          const int j = __shfl(h1.x, i, 64), jp = __shfl(h1.y, i, 64), H = __shfl(h1.z, i, 64);
+          const int t = t_ret_old + i;
+          if (f >= total) continue;
+          const uint32_t w = words[o + r];
+          if (w & ~(live >> 3)) continue;
+          uint64_t keep_lo = ~0ull;
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+            if (fresh & (1u << k)) keep_lo &= keep64(k);
+          PipeStep* st = &ring[t % RING];
+          const OpSel* ops = st->ops + OP_PAD;
+          const uint64_t X = pipe_x(B, w, fresh >> 3, jp, keep_lo);
+          uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+          R = close_in_word(X, w, live, j, ops, foldm, R);
+          B[w] = X | R;
+          expl += (uint32_t)__popcll(R);
+          if (t > 0) st_fout += (uint32_t)__popcll(X);
+          if (X) st->anyx = 1;
+        }
+        segm = 0;
+      }
       int i = segm ? (int)__builtin_ctzll(segm) : -1;
       uint32_t wn = 0;
       if (i >= 0 && (uint32_t)tt < rdl(nq_l, i)) wn = words[rdl(o_l, i) + tt];

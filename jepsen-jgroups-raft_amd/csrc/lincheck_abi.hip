@@ -138,7 +138,7 @@ struct lc_plan {
   int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
   int tile_lbits = DENSE_LMAX;                        // LC_TILE_LBITS: local slots per tile
   int wide_from = 99, wide_lbits = DENSE_LMAX;        // LC_TILE_WIDE=w:b: b local slots from width w
-  int dense_pipe = 1;  // LC_PIPE: bit 0 BLOCK, bit 1 WAVE teams overlap steps (0: one step at a time)
+  int dense_pipe = 3;  // LC_PIPE: bits 0/1/2 = BLOCK/WAVE/TILE teams overlap steps (0: one at a time)
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_w0 = nullptr, ev_w1 = nullptr;  // per dense kernel
