@@ -1171,9 +1171,10 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   TeamCtl* const ctl = (TeamCtl*)p.ctl + team;
   unsigned long long* const flags = p.flags + base;
   const int lb = p.team_lbits[team];  // local slots of every tile (<= DENSE_LMAX)
-  auto mirror = [&](int r) { return p.mirror + ((size_t)(base + r) << HSOLO); };
-  uint64_t* const mine = mirror(rank);
+  int mpar = 0;  // mirror buffer of the current team step (LC_PIPE bit 3: team-step parity)
+  auto mirror = [&](int r) { return p.mirror + ((size_t)(2 * (base + r) + mpar) << HSOLO); };
   auto bar = [&]() { return team_bar(ctl, G, p.abort, &sAbort); };
+  const bool nobar = (p.pipe & 8) != 0;
   unsigned long long expl = 0, stepctr = 0;
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};  // LC_DEBUG phase cycles (wait, compute, publish, return, barrier, steps)
   auto now = []() { return __builtin_amdgcn_s_memrealtime(); };
@@ -1206,6 +1207,21 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   auto team_step = [&](long long hpos) -> bool {
     ++stepctr;
     const unsigned long long tok0 = stepctr << 5;
+    if (nobar) {
+      // double-buffered mirrors: the buffer of step stepctr - 2 is rewritten only after every
+      // tile finished that step (its pulls and return copies read it)
+      mpar = (int)(stepctr & 1);
+      if (stepctr > 2 && tid < 64) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        long spins = 0;
+        for (int r0 = 0; r0 < G; r0 += 64)
+          while (!__all(r0 + lane >= G ||
+                        poll_until(p, &p.done[base + (r0 + lane < G ? r0 + lane : 0)], stepctr - 2, t0, spins)))
+            ;
+      }
+      __syncthreads();
+    }
+    uint64_t* const mine = mirror(rank);
     const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.stream[hpos]);
     const uint32_t live = H0 & 0x3fffffu;
     const int j = (int)((H0 >> 22) & 31u);
@@ -1322,6 +1338,12 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
       ph[3] += now() - tr;
     }
     const unsigned long long tb = now();
+    if (nobar) {  // this tile's survivors only; the verdict is decided after the last step
+      const bool mine_any = __syncthreads_or(anyv != 0);
+      if (tid == 0) st_agent(&p.done[base + rank], stepctr);
+      ph[4] += now() - tb;
+      return mine_any;
+    }
     if (__syncthreads_or(anyv != 0) && tid == 0)
       __hip_atomic_fetch_or(&ctl->any, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bar();  // every tile done with this step (mirrors may be rewritten after this)
@@ -1331,7 +1353,57 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     return sAny != 0;
   };
 
-  if (rank == 0) {  // ---------------------------------------------------------- leader
+  if (nobar) {  // every tile walks the stream; no team barrier per step
+    const int ns = p.nsteps[h];
+    uint32_t* const anyb = p.team_any + p.team_any_off[team];
+    if (p.stamps && rank == 0 && tid == 0) p.stamps[4 * h] = __builtin_amdgcn_s_memrealtime();
+    StreamWin sw;
+    long long pos = p.sbeg[h];
+    unsigned long long team_cycles = 0, team_steps = 0;
+    for (int t = 0; t < ns; ++t) {
+      sw.need(p, pos, lane);
+      int ninv;
+      const uint32_t H0 = read_step(sw, pos, lane, tid < 64, sOp, &ninv);
+      const long long hpos = pos;
+      pos += 1 + ninv;
+      __syncthreads();
+      const uint32_t live = H0 & 0x3fffffu;
+      const int j = (int)((H0 >> 22) & 31u);
+      bool surv = false;
+      if ((live >> lb) == 0) {  // narrow step: the leader alone (other tiles empty)
+        if (rank == 0) {
+          const uint32_t foldm = fold_mask(sOp);
+          expl += run_layers<HSOLO, 4>(sTab, &sZero, p.words, sWOff, sBinom, live, j, sOp, foldm, tid, 1024,
+                                       [] { __syncthreads(); });
+          surv = __syncthreads_or(return_slot(sTab, live, j, tid, 1024, st_fout) != 0);
+        }
+      } else {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        surv = team_step(hpos);
+        team_cycles += __builtin_amdgcn_s_memrealtime() - t0;
+        ++team_steps;
+      }
+      if (surv && tid == 0)
+        __hip_atomic_fetch_or(&anyb[t >> 5], 1u << (t & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();  // the next header rewrites sOp
+    }
+    bar();  // every tile's survivor bits are in
+    if (rank == 0 && tid == 0) {
+      int fail_t = -1;  // the first step after which no tile holds a config
+      for (int t = 0; t < ns && fail_t < 0; ++t)
+        if (!((ld_agent(&anyb[t >> 5]) >> (t & 31)) & 1u)) fail_t = t;
+      p.fail_step[h] = fail_t;
+      p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      st_steps += fail_t >= 0 ? fail_t + 1 : ns;
+      if (p.stamps) {
+        p.stamps[4 * h + 1] = __builtin_amdgcn_s_memrealtime();
+        p.stamps[4 * h + 2] = team_cycles;
+        p.stamps[4 * h + 3] = team_steps;
+      }
+    }
+    const unsigned long long e = block_sum(expl, &sRed);
+    if (tid == 0 && e) atomicAdd(&p.explored[h], e);
+  } else if (rank == 0) {  // ------------------------------------------------- leader
     if (p.stamps && tid == 0) p.stamps[4 * h] = __builtin_amdgcn_s_memrealtime();
     const int ns = p.nsteps[h];
     unsigned long long team_cycles = 0, team_steps = 0;
@@ -1402,6 +1474,14 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   }
   if (p.tstamps && tid == 0)
     for (int i = 0; i < 6; ++i) p.tstamps[blockIdx.x * 8 + i] = ph[i];
+  if (nobar && (p.pipe & 1)) {
+    // the team is done (its final barrier passed, and other tiles read only this tile's HBM
+    // mirror, never its LDS): join the BLOCK queue, whose heaviest-first order leaves the
+    // light tail to late joiners
+    __syncthreads();
+    history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
+                                               st_fout, st_steps);
+  }
   flush_stats(p, st_fout, st_steps, tid == 0);
 }
 

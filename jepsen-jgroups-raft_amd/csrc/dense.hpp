@@ -60,8 +60,10 @@ struct DenseParams {
                                 // (per-step loop only)
   uint32_t* team_any;           // pipelined teams: per team, bit t = some tile read a nonzero
   const int32_t* team_any_off;  // frontier in step t (step ns: the last return); word offsets
-  int32_t pipe;                 // bit 0: BLOCK, bit 1: WAVE, bit 2: TILE teams overlap
-                                // consecutive steps (history_pipe / team_pipe); default 3
+  unsigned long long* done;      // [n_team_wgs] team steps finished (LC_PIPE bit 3)
+  int32_t pipe;                 // bit 3: tile teams without per-step team barriers;
+                                // bit 0: BLOCK, bit 1: WAVE, bit 2: TILE teams overlap
+                                // consecutive steps (history_pipe / team_pipe); default 11
 };
 
 // Kernels: WAVE = 256-thread workgroups, one history per wave (width <= DENSE_WAVE_LMAX);

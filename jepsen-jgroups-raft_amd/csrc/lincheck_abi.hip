@@ -128,7 +128,7 @@ struct lc_plan {
   // dense closure tables (narrow cas-register histories; dense.hpp)
   std::vector<int> dense_b, dense_w, dense_x;  // block / wave / wide teams, heaviest first
   DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dwords, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
-  DevArray d_tany, d_tanyoff;
+  DevArray d_tany, d_tanyoff, d_tdone;
   DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_tlbits, d_thist;
   struct StepBytes { double lds, hbm; };
   std::vector<StepBytes> dalg;     // per dense step: algorithmic bytes
@@ -138,7 +138,9 @@ struct lc_plan {
   int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
   int tile_lbits = DENSE_LMAX;                        // LC_TILE_LBITS: local slots per tile
   int wide_from = 99, wide_lbits = DENSE_LMAX;        // LC_TILE_WIDE=w:b: b local slots from width w
-  int dense_pipe = 3;  // LC_PIPE: bits 0/1/2 = BLOCK/WAVE/TILE teams overlap steps (0: one at a time)
+  // LC_PIPE: bits 0/1/2 = BLOCK/WAVE/TILE teams overlap steps (0: one at a time); bit 3 = tile
+  // teams without per-step team barriers (finished teams then join the BLOCK queue)
+  int dense_pipe = 11;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_w0 = nullptr, ev_w1 = nullptr;  // per dense kernel
@@ -470,7 +472,8 @@ struct lc_plan {
         if (t > DENSE_WIDE_LMAX - DENSE_LMAX) pipe_mode &= ~4;
     p.pipe = pipe_mode;
     if (max_wgs) {
-      const size_t slots = (pipe_mode & 4) ? DENSE_MRING : 1;
+      const size_t slots = (pipe_mode & 4) ? DENSE_MRING : 2;  // 2: the per-step loop's buffers
+      HIP_TRY(d_tdone.ensure(max_wgs * 8));
       HIP_TRY(d_mirror.ensure((max_wgs * slots << (DENSE_LMAX - 3)) * 8));
       HIP_TRY(d_tany.ensure(std::max<size_t>(max_anyw, 1) * 4));
       HIP_TRY(d_tanyoff.ensure(max_teams * 4));
@@ -512,6 +515,8 @@ struct lc_plan {
         HIP_TRY(hipMemcpyAsync(d_tlbits.p, l_lbits[l].data(), nt, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(d_thist.p, l_hist[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemsetAsync(d_tflags.p, 0, (size_t)twgs * 8, stream));
+        HIP_TRY(hipMemsetAsync(d_tdone.p, 0, (size_t)twgs * 8, stream));
+        q.done = d_tdone.as<unsigned long long>();
         HIP_TRY(hipMemsetAsync(d_ctl.p, 0, (size_t)nt * dense_ctl_bytes(), stream));
         HIP_TRY(hipMemcpyAsync(d_tanyoff.p, l_anyoff[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemsetAsync(d_tany.p, 0, std::max<size_t>(max_anyw, 1) * 4, stream));
