@@ -754,6 +754,29 @@ __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
   flush_stats(p, st_fout, st_steps, tt == 0);
 }
 
+// MID teams: one history per 256-thread workgroup, tables of 2^DENSE_MID_LMAX masks (16 KiB),
+// pipelined steps; several workgroups share a CU (BLOCK histories of widths 12..14, whose
+// steps are mostly narrow and latency-bound, no longer hold a whole CU each).
+constexpr int MID_WG = 256, MID_RING = 6;  // LDS <= the wave kernel's (both fit beside a big workgroup)
+__global__ void __launch_bounds__(MID_WG) dense_mid_kernel(DenseParams p) {
+  constexpr int HMAX = DENSE_MID_LMAX - 3;
+  __shared__ uint64_t sTab[1 << HMAX];
+  __shared__ uint32_t sWOff[DENSE_WORD_BITS + 2];
+  __shared__ uint32_t sBinom[BINOM_N * BINOM_N];
+  __shared__ PipeStep sRing[MID_RING];
+  __shared__ int sQ;
+  __shared__ unsigned long long sRed;
+  __shared__ uint64_t sZero;
+  const int tid = threadIdx.x;
+  init_tables(sBinom, sWOff, DENSE_WORD_BITS, MID_WG);
+  if (tid == 0) sZero = 0;
+  __syncthreads();
+  unsigned long long st_fout = 0, st_steps = 0;
+  history_pipe<MID_WG, DENSE_MID_LMAX, MID_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
+                                                 st_fout, st_steps);
+  flush_stats(p, st_fout, st_steps, tid == 0);
+}
+
 // Team barrier over a tile team's G workgroups: every wave drains its (sc1) stores, one lane
 // per workgroup adds to the arrival counter, the last arriver bumps the generation the
 // others poll (relaxed sc1 loads + s_sleep). A 20 s watchdog raises p.abort instead of
@@ -1124,6 +1147,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
 // its layer token (flags[r] = step << 5 | layer + 1), and successors poll the
 // tokens of their predecessors — point-to-point, one hop per team bit, instead of a team
 // barrier per layer. Returning a team slot j: tiles without j take tile r | j's mirror.
+template <bool TEAM_PIPE>
 __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   constexpr int HSOLO = DENSE_LMAX - 3;
   __shared__ uint64_t sTab[1 << HSOLO];
@@ -1152,10 +1176,14 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   unsigned long long st_fout = 0, st_steps = 0;
 
   if ((int)blockIdx.x >= p.n_team_wgs) {  // ------------------------------- BLOCK histories
-    if (p.pipe & 1)
+    if (p.pipe & 1) {
       history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
                                                  st_fout, st_steps);
-    else
+      DenseParams q2 = p;  // then help with the MID queue
+      q2.n = p.n2, q2.order = p.order2, q2.queue = p.queue2;
+      history_pipe<1024, DENSE_LMAX, BLOCK_RING>(q2, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
+                                                 st_fout, st_steps);
+    } else
       history_loop<1024, DENSE_LMAX>(p, sTab, &sZero, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout,
                                      st_steps);
     flush_stats(p, st_fout, st_steps, tid == 0);
@@ -1183,7 +1211,9 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   __syncthreads();
   if (rank == 0 && tid == 0) sTab[0] = 1;  // (cas-register) starts at nil: state id 0
 
-  if (p.pipe & 4) {  // pipelined tile team
+  if constexpr (TEAM_PIPE) {  // pipelined tile team (LC_PIPE bit 2; its own instantiation: it
+    // needs far more scalar registers than the rest, which must leave room beside the
+    // wave / MID workgroups)
     team_pipe(p, sTab, &sZero, sRing, sCum, sBinom, sWOff, team, base, rank, G, h, lb, &sAbort, expl, st_fout);
     bar();  // every tile's survivor bits are in
     if (rank == 0 && tid == 0) {
@@ -1481,6 +1511,10 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     __syncthreads();
     history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
                                                st_fout, st_steps);
+    DenseParams q2 = p;
+    q2.n = p.n2, q2.order = p.order2, q2.queue = p.queue2;
+    history_pipe<1024, DENSE_LMAX, BLOCK_RING>(q2, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
+                                               st_fout, st_steps);
   }
   flush_stats(p, st_fout, st_steps, tid == 0);
 }
@@ -1502,9 +1536,9 @@ int dense_grid_size(DenseTeam kind) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
   int per_cu = 0;
-  hipError_t e = kind == DENSE_WAVE
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_wave_kernel, WAVE_WG, 0)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_big_kernel, 1024, 0);
+  hipError_t e = kind == DENSE_WAVE ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_wave_kernel, WAVE_WG, 0)
+                 : kind == DENSE_MID  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_mid_kernel, MID_WG, 0)
+                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_big_kernel<false>, 1024, 0);
   if (e != hipSuccess || per_cu < 1) return 0;
   // wave teams: one workgroup per CU beside a big-kernel workgroup (whose LDS leaves room);
   // big kernel: one workgroup per CU, so every tile team is resident at once
@@ -1514,8 +1548,12 @@ int dense_grid_size(DenseTeam kind) {
 hipError_t launch_dense(const DenseParams& p, DenseTeam kind, int grid, hipStream_t stream) {
   if (kind == DENSE_WAVE)
     hipLaunchKernelGGL(dense_wave_kernel, dim3(grid), dim3(WAVE_WG), 0, stream, p);
+  else if (kind == DENSE_MID)
+    hipLaunchKernelGGL(dense_mid_kernel, dim3(grid), dim3(MID_WG), 0, stream, p);
+  else if (p.pipe & 4)
+    hipLaunchKernelGGL(dense_big_kernel<true>, dim3(grid), dim3(1024), 0, stream, p);
   else
-    hipLaunchKernelGGL(dense_big_kernel, dim3(grid), dim3(1024), 0, stream, p);
+    hipLaunchKernelGGL(dense_big_kernel<false>, dim3(grid), dim3(1024), 0, stream, p);
   return hipGetLastError();
 }
 

@@ -16,6 +16,7 @@ namespace lc {
 
 constexpr int DENSE_LMAX = 17;       // widest table a workgroup holds in LDS (128 KiB)
 constexpr int DENSE_WAVE_LMAX = 11;  // histories this narrow run one per wave
+constexpr int DENSE_MID_LMAX = 14;   // ... this narrow one per 256-thread workgroup (16 KiB table)
 constexpr int DENSE_WIDE_LMAX = 22;  // widest table a tile team holds (2^(22-17) LDS tiles)
 constexpr int DENSE_MAX_STATES = 8;  // register values (state ids) per history
 constexpr int DENSE_WORD_BITS = DENSE_WIDE_LMAX - 3;  // bits of the sorted word list
@@ -36,6 +37,9 @@ struct DenseParams {
   const uint32_t* stream;
   int64_t stream_words;
   int32_t* queue;               // dequeue counter (zeroed before launch)
+  int32_t n2;                   // BLOCK teams: a second queue drained after the first (the MID
+  const int32_t* order2;        // histories, so a CU whose BLOCK work is done helps there)
+  int32_t* queue2;
   int32_t* status;              // [n_hist] ST_VALID / ST_INVALID
   int32_t* fail_step;           // [n_hist]
   unsigned long long* explored; // [n_hist] (wide teams add into it: zeroed before launch)
@@ -73,7 +77,7 @@ struct DenseParams {
 // LC_DEBUG per-width step profile: steps, step time (100 MHz), nonzero words before the
 // closure, nonzero words after it, configs explored
 constexpr int LH_N = 5;
-enum DenseTeam { DENSE_WAVE = 0, DENSE_BIG = 1 };
+enum DenseTeam { DENSE_WAVE = 0, DENSE_BIG = 1, DENSE_MID = 2 };
 hipError_t launch_dense(const DenseParams& p, DenseTeam kind, int grid, hipStream_t stream);
 int dense_grid_size(DenseTeam kind);
 size_t dense_ctl_bytes();  // per team

@@ -126,7 +126,7 @@ struct lc_plan {
   // keys-kernel per-workgroup storage
   DevArray d_kscratch, d_kspill, d_kspillpos, d_kstatus, d_kfail, d_kexplored;
   // dense closure tables (narrow cas-register histories; dense.hpp)
-  std::vector<int> dense_b, dense_w, dense_x;  // block / wave / wide teams, heaviest first
+  std::vector<int> dense_b, dense_w, dense_x, dense_m;  // block / wave / wide / mid teams, heaviest first
   DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dwords, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
   DevArray d_tany, d_tanyoff, d_tdone;
   DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_tlbits, d_thist;
@@ -134,16 +134,18 @@ struct lc_plan {
   std::vector<StepBytes> dalg;     // per dense step: algorithmic bytes
   std::vector<int64_t> dalg_off;    // [n_hist + 1] first step of each history in dalg
   int64_t dstream_words = 0;
-  int dgrid_b = 0, dgrid_w = 0;
+  int dgrid_b = 0, dgrid_w = 0, dgrid_m = 0;
   int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
   int tile_lbits = DENSE_LMAX;                        // LC_TILE_LBITS: local slots per tile
   int wide_from = 99, wide_lbits = DENSE_LMAX;        // LC_TILE_WIDE=w:b: b local slots from width w
   // LC_PIPE: bits 0/1/2 = BLOCK/WAVE/TILE teams overlap steps (0: one at a time); bit 3 = tile
-  // teams without per-step team barriers (finished teams then join the BLOCK queue)
+  // teams without per-step team barriers (finished teams then join the BLOCK queue); bit 4 =
+  // MID teams for widths 12..14 (needs bit 0)
   int dense_pipe = 11;
-  hipStream_t stream2 = nullptr;
+  hipStream_t stream2 = nullptr, stream3 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_w0 = nullptr, ev_w1 = nullptr;  // per dense kernel
+  hipEvent_t ev_m0 = nullptr, ev_m1 = nullptr, ev_join3 = nullptr;
   bool spill_clean = false, kspill_clean = false;
   // results
   std::vector<int32_t> status, fail_step;
@@ -160,9 +162,11 @@ struct lc_plan {
     if (ev1) hipEventDestroy(ev1);
     if (ev_fork) hipEventDestroy(ev_fork);
     if (ev_join) hipEventDestroy(ev_join);
-    for (hipEvent_t e : {ev_b0, ev_b1, ev_w0, ev_w1})
+    if (ev_join3) hipEventDestroy(ev_join3);
+    for (hipEvent_t e : {ev_b0, ev_b1, ev_w0, ev_w1, ev_m0, ev_m1})
       if (e) hipEventDestroy(e);
     if (stream2) hipStreamDestroy(stream2);
+    if (stream3) hipStreamDestroy(stream3);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -212,13 +216,16 @@ struct lc_plan {
     if (!ev0) HIP_TRY(hipEventCreate(&ev0));
     if (!ev1) HIP_TRY(hipEventCreate(&ev1));
     if (!stream2) HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    if (!stream3) HIP_TRY(hipStreamCreateWithFlags(&stream3, hipStreamNonBlocking));
     if (!ev_fork) HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     if (!ev_join) HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-    for (hipEvent_t* e : {&ev_b0, &ev_b1, &ev_w0, &ev_w1})
+    if (!ev_join3) HIP_TRY(hipEventCreateWithFlags(&ev_join3, hipEventDisableTiming));
+    for (hipEvent_t* e : {&ev_b0, &ev_b1, &ev_w0, &ev_w1, &ev_m0, &ev_m1})
       if (!*e) HIP_TRY(hipEventCreate(e));
     nwg = search_grid_size(model);
     dgrid_b = dense_grid_size(DENSE_BIG);
     dgrid_w = dense_grid_size(DENSE_WAVE);
+    dgrid_m = dense_grid_size(DENSE_MID);
     knwg = keys_grid_size(model);
     if (nwg <= 0 || knwg <= 0) {
       last_error = "search kernels cannot be resident (occupancy 0)";
@@ -312,7 +319,8 @@ struct lc_plan {
     dense_b.clear();
     dense_w.clear();
     dense_x.clear();
-    if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0) return 0;
+    dense_m.clear();
+    if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0 || dgrid_m <= 0) return 0;
     const int n = enc.n_hist;
     std::vector<uint32_t> words;
     std::vector<int64_t> sbeg(n, 0);
@@ -346,15 +354,19 @@ struct lc_plan {
         dalg.push_back(step_alg_bytes(live, (int)(q1 - q0)));
       }
       const int lw = enc.live_max[h];
-      (lw <= DENSE_WAVE_LMAX ? dense_w : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
+      // MID teams (several per CU) take the narrower BLOCK histories when BLOCK steps are pipelined
+      (lw <= DENSE_WAVE_LMAX ? dense_w : (lw <= DENSE_MID_LMAX && (dense_pipe & 17) == 17) ? dense_m
+       : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
     }
     auto heavy_first = [&](int a, int b) { return cost[a] > cost[b]; };
     std::stable_sort(dense_b.begin(), dense_b.end(), heavy_first);
     std::stable_sort(dense_w.begin(), dense_w.end(), heavy_first);
     std::stable_sort(dense_x.begin(), dense_x.end(), heavy_first);
+    std::stable_sort(dense_m.begin(), dense_m.end(), heavy_first);
     std::vector<int32_t> ord(dense_b.begin(), dense_b.end());
     ord.insert(ord.end(), dense_w.begin(), dense_w.end());
     ord.insert(ord.end(), dense_x.begin(), dense_x.end());
+    ord.insert(ord.end(), dense_m.begin(), dense_m.end());
     dalg_off[n] = (int64_t)dalg.size();
     dstream_words = (int64_t)words.size();
     int rc;
@@ -380,7 +392,8 @@ struct lc_plan {
   // teams do not fit one launch (tile_cap workgroups) run in further big-kernel launches.
   int run_dense(float* ms) {
     const int nb = (int)dense_b.size(), nw = (int)dense_w.size(), nx = (int)dense_x.size();
-    if (nb + nw + nx == 0) return 0;
+    const int nm = (int)dense_m.size();
+    if (nb + nw + nx + nm == 0) return 0;
     const int n = enc.n_hist;
     HIP_TRY(d_stats.ensure(SS_N * 8));
     HIP_TRY(hipMemsetAsync(d_dqueue.p, 0, 16, stream));
@@ -500,6 +513,22 @@ struct lc_plan {
       HIP_TRY(hipEventRecord(ev_w1, stream2));
       HIP_TRY(hipEventRecord(ev_join, stream2));
     }
+    if (nm) {
+      if (!nw) HIP_TRY(hipEventRecord(ev_fork, stream));
+      HIP_TRY(hipStreamWaitEvent(stream3, ev_fork, 0));
+      DenseParams q = p;
+      q.n = nm;
+      q.order = d_dorder.as<int32_t>() + nb + nw + nx;
+      q.queue = d_dqueue.as<int32_t>() + 2;
+      HIP_TRY(hipEventRecord(ev_m0, stream3));
+      // wave + MID workgroups stay within one per CU: either fits beside a big-kernel
+      // workgroup, two of them do not, and every tile-team workgroup must be resident
+      const int wgrid = nw ? std::min(dgrid_w, (nw + 3) / 4) : 0;
+      const int mgrid = std::min(nm, dgrid_m - wgrid);
+      if (mgrid > 0) HIP_TRY(launch_dense(q, DENSE_MID, mgrid, stream3));
+      HIP_TRY(hipEventRecord(ev_m1, stream3));
+      HIP_TRY(hipEventRecord(ev_join3, stream3));
+    }
     HIP_TRY(hipEventRecord(ev_b0, stream));
     for (size_t l = 0; l < launches.size(); ++l) {
       const int nt = (int)l_base[l].size(), twgs = (int)l_wgteam[l].size();
@@ -507,6 +536,9 @@ struct lc_plan {
       q.n = l == 0 ? nb : 0;
       q.order = d_dorder.as<int32_t>();
       q.queue = d_dqueue.as<int32_t>();
+      q.n2 = l == 0 ? nm : 0;
+      q.order2 = d_dorder.as<int32_t>() + nb + nw + nx;
+      q.queue2 = d_dqueue.as<int32_t>() + 2;
       q.n_team_wgs = twgs;
       if (nt) {
         HIP_TRY(hipMemcpyAsync(d_wgteam.p, l_wgteam[l].data(), twgs * 4, hipMemcpyHostToDevice, stream));
@@ -537,11 +569,12 @@ struct lc_plan {
           q.tstamps = d_tstamps.as<unsigned long long>();
         }
       }
-      const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n));
+      const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n + q.n2));
       if (grid > 0) HIP_TRY(launch_dense(q, DENSE_BIG, grid, stream));
     }
     HIP_TRY(hipEventRecord(ev_b1, stream));
     if (nw) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
+    if (nm) HIP_TRY(hipStreamWaitEvent(stream, ev_join3, 0));
     HIP_TRY(hipEventRecord(ev1, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     float t = 0;
@@ -562,27 +595,29 @@ struct lc_plan {
     HIP_TRY(hipMemcpy(ex.data(), d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost));
     unsigned long long ss[SS_N];
     HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
-    for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x})
+    for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
       for (int h : *ids) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
-    stats[1] += (nw ? 1 : 0) + (double)launches.size();
-    stats[12] += nb + nw + nx;
+    stats[1] += (nw ? 1 : 0) + (nm ? 1 : 0) + (double)launches.size();
+    stats[12] += nb + nw + nx + nm;
     stats[13] += t;
     // per-kernel time (events on each kernel's own stream) and algorithmic bytes of the steps
     // each kernel ran: 14/15 big/wave ms, 16/17 big HBM/LDS bytes, 18/19 wave HBM/LDS bytes
     float tb = 0, tw = 0;
     HIP_TRY(hipEventElapsedTime(&tb, ev_b0, ev_b1));
     if (nw) HIP_TRY(hipEventElapsedTime(&tw, ev_w0, ev_w1));
+    float tm = 0;  // the MID kernel runs beside both; its steps are counted with the wave kernel's
+    if (nm) HIP_TRY(hipEventElapsedTime(&tm, ev_m0, ev_m1));
     stats[14] += tb;
-    stats[15] += tw;
-    for (const std::vector<int>* ids : {&dense_b, &dense_x, &dense_w})
+    stats[15] += std::max(tw, tm);
+    for (const std::vector<int>* ids : {&dense_b, &dense_x, &dense_w, &dense_m})
       for (int h : *ids) {
         const StepBytes b = dense_hist_bytes(h, fs[h]);
-        const int k = ids == &dense_w ? 18 : 16;
+        const int k = (ids == &dense_w || ids == &dense_m) ? 18 : 16;
         stats[k] += b.hbm;
         stats[k + 1] += b.lds;
       }
     stats[2] += (double)ss[SS_STEPS];
-    stats[4] += (double)ss[SS_FOUT] + (nb + nw + nx);  // frontier in = previous frontier out (+ initial)
+    stats[4] += (double)ss[SS_FOUT] + (nb + nw + nx + nm);  // frontier in = previous frontier out (+ initial)
     stats[6] += (double)ss[SS_FOUT];
     if (debug()) {
       fprintf(stderr, "[lincheck] dense: %d block + %d wave + %d tile-team histories (%zu launch(es), %zu team "
@@ -622,12 +657,12 @@ struct lc_plan {
     const int n = enc.n_hist;
     std::vector<unsigned long long> T((size_t)n * 4);
     if (hipMemcpy(T.data(), d_dstamps.p, T.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const std::vector<int>* lists[3] = {&dense_b, &dense_w, &dense_x};
-    const char* names[3] = {"block", "wave", "wide"};
+    const std::vector<int>* lists[4] = {&dense_b, &dense_w, &dense_x, &dense_m};
+    const char* names[4] = {"block", "wave", "wide", "mid"};
     unsigned long long t0 = ~0ull;
     for (auto* ids : lists)
       for (int h : *ids) t0 = std::min(t0, T[4 * h]);
-    for (int team = 0; team < 3; ++team) {
+    for (int team = 0; team < 4; ++team) {
       const std::vector<int>& ids = *lists[team];
       if (ids.empty()) continue;
       unsigned long long first = ~0ull, last = 0;
@@ -976,7 +1011,8 @@ struct lc_plan {
     int rc = 0;
     std::vector<int> grid_ids;
     const bool keys = max_t == INT32_MAX && path == 1;
-    const bool dense = max_t == INT32_MAX && path == 0 && (dense_b.size() + dense_w.size() + dense_x.size()) > 0;
+    const bool dense = max_t == INT32_MAX && path == 0 &&
+                       (dense_b.size() + dense_w.size() + dense_x.size() + dense_m.size()) > 0;
     std::vector<char> done(enc.n_hist, 0);
     if (dense) {
       rc = run_dense(&ms);
@@ -984,6 +1020,7 @@ struct lc_plan {
       for (int h : dense_b) done[h] = 1;
       for (int h : dense_w) done[h] = 1;
       for (int h : dense_x) done[h] = 1;
+      for (int h : dense_m) done[h] = 1;
     }
     if (keys) {
       rc = run_keys(&ms);
