@@ -332,12 +332,13 @@ def test_gpu_dense_tables_vs_oracle():
     p.close()
 
 
-@pytest.mark.parametrize("pipe", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "27"])
 def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     """LC_PIPE bit 0 / bit 1: BLOCK / WAVE teams overlap consecutive RETURN steps (step t+1's
     layer q beside step t's layer q + 2, returns read through the previous step's slot, fresh
     slots masked). Every mode is bit-exact with the oracle, invalid histories included (the
-    failing step is found from the next step's empty frontier)."""
+    failing step is found from the next step's empty frontier). 11 adds barrier-free tile teams
+    (the default), 27 also MID teams (widths 12..14 on 256-thread workgroups)."""
     monkeypatch.setenv("LC_PIPE", pipe)
     hs = [synth.gen_register_keys(24, 600, 5, 0.01, config_id=3, invalid_keys=(1, 7, 16))]
     hs += [synth.gen_register(120, 5, 0.1, 33000 + t, invalid=(t % 2 == 1)) for t in range(8)]
@@ -395,6 +396,20 @@ def test_gpu_dense_tile_teams(cap, monkeypatch):
         assert s["launches"] >= h.n_hist  # one launch per team
     for k in range(h.n_hist):
         _cmp(got, exp[k], k, f"tile cap={cap} w={widths[k]}")
+    p.close()
+
+
+def test_gpu_dense_tile_teams_with_step_barriers(monkeypatch):
+    """LC_PIPE=3: the tile-team loop with a leader command and a team barrier per team step
+    (the default, bit 3, drops both and decides survivors from per-step bits after the last
+    step): same answers."""
+    monkeypatch.setenv("LC_PIPE", "3")
+    h, widths, exp = _wide_batch()
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    got = p.results()
+    for k in range(h.n_hist):
+        _cmp(got, exp[k], k, f"barrier team loop w={widths[k]}")
     p.close()
 
 
