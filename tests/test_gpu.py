@@ -413,6 +413,20 @@ def test_gpu_dense_tile_teams_with_step_barriers(monkeypatch):
     p.close()
 
 
+@pytest.mark.parametrize("lbits", ["16", "15", "14"])
+def test_gpu_dense_tile_teams_small_tiles(lbits, monkeypatch):
+    """The default (barrier-free) tile-team loop with smaller tiles: up to 2^8 workgroups per
+    team, so the "every tile finished step s - 2" check spans several 64-lane chunks."""
+    monkeypatch.setenv("LC_TILE_LBITS", lbits)
+    h, widths, exp = _wide_batch()
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    got = p.results()
+    for k in range(h.n_hist):
+        _cmp(got, exp[k], k, f"small tiles lbits={lbits} w={widths[k]}")
+    p.close()
+
+
 @pytest.mark.parametrize("lbits", [None, "15"])
 def test_gpu_dense_tile_teams_pipelined(lbits, monkeypatch):
     """LC_PIPE bit 2: tile teams overlap steps (team_pipe: per-step mirror slots, super-layer
