@@ -8,9 +8,10 @@
 //   for hi-layer q = 0..H (words w with popcount(w) = q, H = width - 3), in parallel:
 //     j hi and j ∈ w : R = T_j(B[w \ j])                 (configs holding j are never expanded)
 //     otherwise      : R = ∪_{k ∈ w} T_k(B[w \ k])        (pulls from finalized words)
-//                      then the in-word closure over the low 3 bits: nlo passes of every live
-//                      low op k ≠ j (R |= T_k((X | R) at positions without k, j) moved up
-//                      by 2^k), and, when j is a low bit, one final j pass into the j positions
+//                      then the in-word closure over the low 3 bits: the live low ops k ≠ j
+//                      in a sequence holding every ordering of them as a subsequence
+//                      (R |= T_k((X | R) at positions without k, j) moved up by 2^k), and,
+//                      when j is a low bit, one final j pass into the j positions
 //     explored += popcount(R);  B[w] = X | R
 //   return j: B'[m] = B[m ∪ j] for m ∌ j, B'[m ∪ j] = 0   (post-return frontier)
 //   B' empty => not linearizable at this RETURN.
@@ -178,16 +179,28 @@ __device__ __forceinline__ uint64_t close_in_word(uint64_t X, uint32_t w, uint32
     const uint32_t notj = j_lo ? keep8(j) : 0xffu;
     const uint64_t notj64 = j_lo ? keep64(j) : ~0ull;
     R &= notj64;  // configs holding j come only from T_j
-    // ---- in-word closure: nlo passes over the live low ops other than j
+    // ---- in-word closure over the live low ops other than j. Transfers accumulate, so a
+    // sequence of ops reaches every config whose chain of low ops is a subsequence of it: the
+    // ops in increasing order, then (two ops a < b) a again, or (three ops) 0 1 0 2 — the
+    // shortest sequences holding every ordering (3 and 7 transfers instead of 4 and 9 passes).
     const uint32_t lo_ops = live & 7u & ~(j_lo ? (1u << j) : 0u);
     const int nlo = __popc(lo_ops);
     const OpSel lo_sel[3] = {ops[0], ops[1], ops[2]};
-    for (int pass = 0; pass < nlo; ++pass) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        if (lo_ops & (1u << k))
-          R |= transfer_lo(lo_sel[k], (foldm >> k) & 1u, X | R, keep8(k) & notj, keep64(k) & notj64, 1 << k);
-      }
+    auto lo_step = [&](int k) {
+      if (lo_ops & (1u << k))
+        R |= transfer_lo(lo_sel[k], (foldm >> k) & 1u, X | R, keep8(k) & notj, keep64(k) & notj64, 1 << k);
+    };
+    lo_step(0);
+    lo_step(1);
+    lo_step(2);
+    if (nlo == 3) {
+      lo_step(0);
+      lo_step(1);
+      lo_step(0);
+      lo_step(2);
+    } else if (nlo == 2) {
+      if (lo_ops & 1u) lo_step(0);
+      else lo_step(1);
     }
     if (j_lo)  // the returning op, linearized last
       R |= transfer_lo(ops[j], (foldm >> j) & 1u, X | R, notj, notj64, 1 << j);
