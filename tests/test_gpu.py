@@ -356,6 +356,54 @@ def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     p.close()
 
 
+def _low_slot_rounds(n_rounds, seed, perturb=False):
+    """Rounds of four overlapping calls: slots 0..2 and 3 invoked together, slot 3 returns
+    first (a hi-bit RETURN with all three low ops live), then 0..2 in a random order. Writes,
+    cas and reads over values 0..2 take effect in a random permutation of the round, so the
+    in-word closure must reach every ordering of the three low ops (writes are OR-folds)."""
+    rng = random.Random(seed)
+    ops, val = [], None
+    for _ in range(n_rounds):
+        calls = []
+        for p in range(4):
+            f = rng.choice(["write", "cas", "read", "write"])
+            calls.append([p, f, rng.randrange(3) if f == "write" else [rng.randrange(3), rng.randrange(3)] if f == "cas" else None])
+        for p, f, v in calls:
+            ops.append({"process": p, "type": "invoke", "f": f, "value": v})
+        done = {}
+        for i in rng.sample(range(4), 4):  # the linearization order of this round
+            p, f, v = calls[i]
+            if f == "write":
+                val, done[p] = v, ("ok", v)
+            elif f == "read":
+                done[p] = ("ok", val)
+            else:
+                ok = val == v[0]
+                if ok:
+                    val = v[1]
+                done[p] = ("ok" if ok else "fail", v)
+        for p in [3] + rng.sample(range(3), 3):
+            t, v = done[p]
+            if perturb and calls[p][1] == "read" and t == "ok" and rng.random() < 0.3:
+                v = ((v if v is not None else -1) + 1) % 3
+            ops.append({"process": p, "type": t, "f": calls[p][1], "value": v})
+    return H.encode(ops)
+
+
+@pytest.mark.parametrize("pipe", ["0", "11"])
+def test_gpu_dense_low_slot_orderings(pipe, monkeypatch):
+    """The in-word closure's op sequence (0 1 2 0 1 0 2 for three live low ops, a b a for two):
+    RETURNs of slot 3 with slots 0..2 pending, writes among them; bit-exact with the oracle,
+    perturbed variants included, through the WAVE teams' per-step and pipelined loops."""
+    monkeypatch.setenv("LC_PIPE", pipe)
+    h = H.concat([_low_slot_rounds(60, 71000 + t, perturb=(t % 2 == 1)) for t in range(16)])
+    exp = oracle.check_many("cas-register", h, n_threads=8)
+    assert any(e["valid"] == 0 for e in exp) and any(e["valid"] == 1 for e in exp)
+    g = _lib.check(1, 0, h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, "low-slot orderings")
+
+
 _WIDE = {}
 
 
