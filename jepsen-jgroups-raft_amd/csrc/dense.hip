@@ -169,6 +169,31 @@ __device__ __forceinline__ uint64_t pull_hi(const uint64_t* B, const uint64_t* z
   return R;
 }
 
+// pull_hi over the batches b0 = bfirst, bfirst + bstep, ... only: a word's pulls split over
+// the lanes of a group (run_layers' narrow layers), OR-combined by the caller.
+__device__ __forceinline__ uint64_t pull_hi_part(const uint64_t* B, const uint64_t* zero, uint32_t w, int j, int H,
+                                                const OpSel* ops, uint32_t foldm, int bfirst, int bstep) {
+  const uint32_t jh = j < 3 ? 0u : 1u << (j - 3);
+  const uint32_t pm = (w & jh) ? jh : w;
+  uint64_t R = 0;
+  for (int b0 = bfirst; b0 < H; b0 += bstep) {
+    const uint4* op4 = reinterpret_cast<const uint4*>(__builtin_assume_aligned(&ops[b0 + 3], 16));
+    const uint4 s01 = op4[0], s23 = op4[1];
+    uint64_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t bit = 1u << (b0 + u);
+      v[u] = *((pm & bit) ? &B[w ^ bit] : zero);
+    }
+    asm volatile("" ::"v"(s01.x), "v"(s01.y), "v"(s01.z), "v"(s01.w), "v"(s23.x), "v"(s23.y), "v"(s23.z),
+                 "v"(s23.w));
+    const OpSel sel[4] = {{s01.x, s01.y}, {s01.z, s01.w}, {s23.x, s23.y}, {s23.z, s23.w}};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) R |= transfer(sel[u], (foldm >> (b0 + u + 3)) & 1u, v[u]);
+  }
+  return R;
+}
+
 // The rest of word w's closure, given R = its pulls (hi bits and other tiles): the in-word
 // closure over the 3 low bits, then the store. Returns popcount(R); *out = X | R.
 __device__ __forceinline__ uint64_t close_in_word(uint64_t X, uint32_t w, uint32_t live, int j, const OpSel* ops,
@@ -245,12 +270,30 @@ __device__ __forceinline__ unsigned long long run_layers(uint64_t* B, const uint
   uint32_t o = __builtin_amdgcn_readfirstlane(wofs[0]);
   uint32_t wn = (uint32_t)tt < nq ? words[o + tt] : 0u;
   for (int q = 0; q <= H; ++q) {
-    for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)nt) {
-      const uint32_t w = wn;
-      if (r + nt < nq) wn = words[o + r + nt];
-      if (w & ~live_hi) continue;
-      uint64_t nv;
-      expl += close_word<HMAX, BATCH>(B, zero, w, live, j, H, ops, foldm, 0ull, &nv);
+    // a layer of at most nt/2 (nt/4) words with two or more pull batches: each word's batches
+    // go to a group of 2 (4) lanes, OR-combined by shuffles, and the group's first lane
+    // finishes the word (every lane reaches the shuffles: inactive sources read 0)
+    const int split = H <= 4 ? 1 : (int)nq * 4 <= nt ? 4 : (int)nq * 2 <= nt ? 2 : 1;
+    if (split > 1) {
+      const int sub = tt & (split - 1);
+      const uint32_t r = (uint32_t)tt / (uint32_t)split;
+      const uint32_t w = r < nq ? words[o + r] : ~0u;
+      const bool act = r < nq && !(w & ~live_hi);
+      uint64_t R = act ? pull_hi_part(B, zero, w, j, H, ops, foldm, 4 * sub, 4 * split) : 0ull;
+      R |= (uint64_t)__shfl_xor((unsigned long long)R, 1, 64);
+      if (split == 4) R |= (uint64_t)__shfl_xor((unsigned long long)R, 2, 64);
+      if (act && sub == 0) {
+        uint64_t nv;
+        expl += finish_word(B, w, live, j, ops, foldm, R, &nv);
+      }
+    } else {
+      for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)nt) {
+        const uint32_t w = wn;
+        if (r + nt < nq) wn = words[o + r + nt];
+        if (w & ~live_hi) continue;
+        uint64_t nv;
+        expl += close_word<HMAX, BATCH>(B, zero, w, live, j, H, ops, foldm, 0ull, &nv);
+      }
     }
     if (q < H) {
       nq = __builtin_amdgcn_readfirstlane(binom[H * BINOM_N + q + 1]);
