@@ -1339,17 +1339,32 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
         static_assert(TW * 1024 >= 3432, "a layer of a 17-bit tile fits TW words per thread");
         uint32_t wl[TW];
         uint64_t R0[TW];
+        // a layer of at most 512 (256) words: word rr belongs to a group of 2 (4) lanes that
+        // split its local pull batches (as in run_layers); the group's first lane goes on
+        const int split = H <= 4 ? 1 : (int)nq * 4 <= 1024 ? 4 : (int)nq * 2 <= 1024 ? 2 : 1;
+        const int sub = tid & (split - 1);
+        const uint32_t rr = (uint32_t)tid / (uint32_t)split;
 #pragma unroll
         for (int k = 0; k < TW; ++k) {
-          const uint32_t r = (uint32_t)tid + (uint32_t)k * 1024u;
+          const uint32_t r = rr + (uint32_t)k * 1024u;
           wl[k] = r < nq ? p.words[o + r] : ~0u;  // ~0u: no word (fails the live test)
           R0[k] = 0;
         }
         // the hi-bit pulls read only this tile's finished layers: done before waiting for the
         // predecessors' layer q (a tile holding j pulls nothing locally)
+        if (split > 1) {
+          uint64_t R = (!tile_j && !(wl[0] & ~live_hi))
+                           ? pull_hi_part(sTab, &sZero, wl[0], j, H, sOp, foldm, 4 * sub, 4 * split)
+                           : 0ull;
+          R |= (uint64_t)__shfl_xor((unsigned long long)R, 1, 64);
+          if (split == 4) R |= (uint64_t)__shfl_xor((unsigned long long)R, 2, 64);
+          R0[0] = R;
+          if (sub) wl[0] = ~0u;
+        } else {
 #pragma unroll
-        for (int k = 0; k < TW; ++k)
-          if (!tile_j && !(wl[k] & ~live_hi)) R0[k] = pull_hi<4>(sTab, &sZero, wl[k], j, H, sOp, foldm);
+          for (int k = 0; k < TW; ++k)
+            if (!tile_j && !(wl[k] & ~live_hi)) R0[k] = pull_hi<4>(sTab, &sZero, wl[k], j, H, sOp, foldm);
+        }
         {
           const unsigned long long tw = now();
           wait_flags(p, flags, rank, preds, tok0 + q + 1, &sAbort);
@@ -1360,7 +1375,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
           const int b = __builtin_ctz(m);
           const OpSel sb = sOp[lb + b];
           const bool fb = (foldm >> (lb + b)) & 1u;
-          const uint64_t* src = mirror(rank ^ (1 << b)) + mo + tid;
+          const uint64_t* src = mirror(rank ^ (1 << b)) + mo + rr;
           uint64_t v[TW];
 #pragma unroll
           for (int k = 0; k < TW; ++k) {
@@ -1386,7 +1401,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
           } else {
             expl += finish_word(sTab, w, live_loc, j, sOp, foldm, R0[k], &nv);
           }
-          HbmTab::st(mine + mo + tid + k * 1024, nv);  // mirrors are in word-list order
+          HbmTab::st(mine + mo + rr + k * 1024, nv);  // mirrors are in word-list order
         }
         mo += nq;
         __syncthreads();
