@@ -5,8 +5,9 @@ verified/sec + configs explored/sec, % of the HBM roofline).
 One "step" = one full check of the workload's histories by the HIP search (lc_plan_run on
 HBM-resident encoded histories). Default workload: C3 (jepsen.independent cas-register,
 1k keys x 1k ops, 5 clients/key, p_info 0.01), the north_star's headline config; under
-`torchrun --nproc-per-node N` every rank checks its own 1k-key shard (weak scaling,
-no data-path collective: keys are independent, SURVEY §8(e) axis 1).
+`torchrun --nproc-per-node N` the 1k keys are split over the ranks (strong scaling, as
+BASELINE configs[2] says; no data-path collective: keys are independent, SURVEY §8(e) axis
+1). `end_to_end` times lc_check from host arrays (encode + H2D + search + D2H).
 
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` and `cpu_baseline`.
 """
@@ -17,6 +18,8 @@ import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jepsen-jgroups-raft_amd"))
@@ -237,6 +240,46 @@ def bench_partition(args, rank, world, dist, barrier_sync):
     }
 
 
+def cpu_info():
+    """Host CPU facts for cpu_baseline: model name, nproc, the affinity set, and the thread
+    count used = the box's CPU share per GPU (OMP_NUM_THREADS, 16 on the GPU box) or, when
+    unset, every CPU this process may run on."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
+    return {"cpu_model": model, "nproc": nproc, "affinity": aff, "threads": max(1, threads),
+            "share": "OMP_NUM_THREADS" if omp.isdigit() else "affinity"}
+
+
+def read_profile(path, workload, scale, kname):
+    """Per-launch PMC figures committed under profiles/ (tools/pmc_traffic.py) for this
+    workload and kernel, or None."""
+    if not os.path.exists(path):
+        return None
+    try:
+        tr = json.load(open(path))
+    except Exception:  # noqa: BLE001
+        return None
+    if tr.get("workload") != workload or abs(tr.get("scale", 1.0) - scale) > 1e-9:
+        return None
+    if tr.get("kernel", "") not in kname:
+        return None
+    return tr
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -246,6 +289,10 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e-reps", type=int, default=3,
+                    help="lc_check calls from host arrays timed after the run (0: skip)")
+    ap.add_argument("--emulate", default="",
+                    help="r/N: check rank r's share of an N-rank split on this one GPU")
     ap.add_argument("--partition", action="store_true",
                     help="axis 2: one history (c2/c4) with its frontier partitioned over ranks")
     ap.add_argument("--capacity-log2", type=int, default=0, help="--partition: per-rank capacity")
@@ -283,16 +330,25 @@ def main():
     model = MODEL_OF[args.workload]
     kind = _lib.MODEL_KIND[model]
     cfg = synth.CONFIGS[args.workload]
-    # weak scaling: rank r checks keys [r*K, (r+1)*K) (distinct seeds per key)
-    n_keys = cfg["n_keys"] if cfg["n_keys"] == 1 else max(1, int(cfg["n_keys"] * args.scale))
+    # strong scaling (BASELINE configs[2]: 1k keys sharded across the GPUs): every rank builds
+    # the same key set and keeps its share of lc_shard_histories' LPT split, the split
+    # lc_check(n_gpus) uses; keys are independent, so no data-path collective
     t0 = time.perf_counter()
-    h = synth.gen_config(args.workload, key0=rank * n_keys, scale=args.scale)
+    h_all = synth.gen_config(args.workload, scale=args.scale)
+    shard_rank, shard_world = rank, world
+    if args.emulate:
+        shard_rank, shard_world = (int(x) for x in args.emulate.split("/"))
+    if shard_world > 1 and h_all.n_hist > 1:
+        mine = np.flatnonzero(_lib.shard_histories(h_all, shard_world) == shard_rank)
+        h = h_all.select(mine.tolist())
+    else:
+        h = h_all
     gen_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     plan = _lib.Plan(kind, 0, h, device=local)
     plan_s = time.perf_counter() - t0
-    log(f"[rank {rank}] {args.workload}: {h.n_hist} histories, {h.n} entries, "
-        f"{h.n_ops()} ops; gen {gen_s:.2f}s, encode+upload {plan_s:.2f}s")
+    log(f"[rank {rank}] {args.workload}: {h.n_hist} of {h_all.n_hist} histories, {h.n} entries, "
+        f"{h.n_ops()} ops; gen {gen_s:.2f}s, plan create (encode+upload) {plan_s:.2f}s")
 
     for _ in range(args.warmup):
         plan.run()
@@ -313,13 +369,36 @@ def main():
         elapsed = float(t.item())
     res = plan.results()
     st = plan.stats()
-    ops_rank = h.n_ops()
+    phases = {k[len("create_"):]: round(st[k], 3) for k in st if k.startswith("create_")}
+    log(f"[rank {rank}] plan create phases (ms): {phases}")
     explored_rank = int(res["explored"].sum())
-    total_ops = ops_rank * world * args.steps
-    total_cfg = explored_rank * world * args.steps
+    total_ops = h_all.n_ops() * args.steps if not args.emulate else h.n_ops() * args.steps
     value = total_ops / elapsed
     vcount = {int(v): int((res["valid"] == v).sum()) for v in (0, 1, 2)}
+    plan.close()
 
+    # end to end through the C-ABI as a JVM caller uses it (lc_check: host arrays -> encode
+    # (a4/a8) -> H2D -> search -> D2H), rank 0's share; PCIe-inclusive, so never `value`
+    e2e = None
+    if args.e2e_reps > 0 and rank == 0:
+        ts = []
+        for _ in range(args.e2e_reps):
+            t0 = time.perf_counter()
+            _lib.check(kind, 0, h)
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        med = ts[len(ts) // 2]
+        e2e = {"ms_per_check": med * 1e3, "value": h.n_ops() / med, "unit": "history ops/s",
+               "reps": args.e2e_reps, "what": "lc_check from host arrays (encode + H2D + search "
+               "+ D2H), this rank's histories", "plan_create_phases_ms": phases}
+
+    if dist:
+        # every rank's explored configs (the whole job's configs/s)
+        t = dist[0].tensor([explored_rank], dtype=dist[0].int64, device="cuda")
+        dist[1].all_reduce(t)
+        explored_all = int(t.item())
+    else:
+        explored_all = explored_rank
     if rank != 0:
         if dist:
             dist[1].destroy_process_group()
@@ -327,53 +406,65 @@ def main():
 
     # dominant kernel: the dense closure-table kernels when they decided histories (events on
     # each kernel's own stream), else the grid search kernel
-    dense = {k: 0.0 for k in ("dense_big_ms", "dense_wave_ms", "dense_big_hbm_bytes",
-                              "dense_big_lds_bytes", "dense_wave_hbm_bytes", "dense_wave_lds_bytes")}
+    acc = {}
     for s_ in step_stats:
-        for k in dense:
-            dense[k] += s_[k]
+        for k, v in s_.items():
+            acc[k] = acc.get(k, 0.0) + v
+    avg = {k: v / args.steps for k, v in acc.items()}
     if st["dense_histories"] > 0:
-        which = "big" if dense["dense_big_ms"] >= dense["dense_wave_ms"] else "wave"
+        which = "big" if avg["dense_big_ms"] >= avg["dense_wave_ms"] else "wave"
         kname = f"lc::dense_{which}_kernel"
-        k_s = dense[f"dense_{which}_ms"] / args.steps / 1e3
-        alg_bytes = dense[f"dense_{which}_hbm_bytes"] / args.steps
-        lds_bytes = dense[f"dense_{which}_lds_bytes"] / args.steps
+        k_ms = avg[f"dense_{which}_ms"]
+        fin, fout, expl = (avg[f"dense_{which}_{q}"] for q in ("frontier_in", "frontier_out",
+                                                                "explored"))
+        table_hbm = avg[f"dense_{which}_hbm_bytes"]
+        lds_bytes = avg[f"dense_{which}_lds_bytes"]
     else:
         kname = "lc::search_kernel"
-        k_s = kernel_ms / args.steps / 1e3
-        alg_bytes = st["alg_bytes"]  # per launch set (one step)
-        lds_bytes = None
-    achieved = alg_bytes / k_s / 1e9 if k_s > 0 else 0.0
-    traffic = None
-    if os.path.exists(args.traffic):
-        try:
-            tr = json.load(open(args.traffic))
-            if (tr.get("workload") == args.workload and abs(tr.get("scale", 1.0) - args.scale) < 1e-9
-                    and tr.get("kernel", "") in kname):
-                traffic = tr.get("hbm_bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
+        k_ms = kernel_ms / args.steps
+        fin, fout, expl = st["frontier_in"], st["frontier_out"], st["candidates"]
+        table_hbm = lds_bytes = None
+    # bytes_alg = F_in*C + N_cand*(C+8) + F_out*C (C = 8 B per register config);
+    # the dense kernels do not enumerate candidates, so N_cand is taken as the configs they
+    # produced (every new config is at least one consistent candidate): a lower bound
+    C = st["config_bytes"] or 8.0
+    alg = fin * C + expl * (C + 8) + fout * C
+    k_s = k_ms / 1e3
+    achieved = alg / k_s / 1e9 if k_s > 0 else 0.0
+    prof = read_profile(args.traffic, args.workload, args.scale, kname)
+    traffic = prof.get("hbm_bytes_per_launch") if prof else None
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
-            "kernel_ms": k_s * 1e3, "alg_bytes_per_launch": alg_bytes}
-    if lds_bytes is not None:
+            "kernel_ms": k_ms, "alg_bytes_per_launch": alg,
+            "alg_model": "SURVEY 8(d): F_in*C + N_cand*(C+8) + F_out*C, C=8; N_cand >= "
+                         "configs explored (lower bound)" if table_hbm is not None else
+                         "SURVEY 8(d): F_in*C + N_cand*(C+8) + F_out*C",
+            "terms": {"frontier_in": fin, "n_cand": expl, "frontier_out": fout}}
+    if table_hbm is not None:
         lds_ach = lds_bytes / k_s / 1e9 if k_s > 0 else 0.0
-        roof["lds"] = {"achieved": lds_ach, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-                       "frac": lds_ach / LDS_PEAK_GBS, "alg_bytes_per_launch": lds_bytes}
-        roof["note"] = ("closure tables live in LDS: HBM carries only the step streams and tile "
-                        "mirrors, so the HBM fraction is small by design; the kernel's time is "
-                        "the longest history's dependent chain of popcount layers (VALU issue "
-                        "and LDS latency), see DESIGN.md §3.1")
+        roof["table"] = {"hbm_bytes_per_launch": table_hbm, "lds_bytes_per_launch": lds_bytes,
+                         "lds_achieved": lds_ach, "lds_peak": LDS_PEAK_GBS, "unit": "GB/s",
+                         "lds_frac": lds_ach / LDS_PEAK_GBS,
+                         "note": "what the closure tables really move: step streams + tile "
+                                 "mirrors in HBM, the tables themselves in LDS"}
+        if prof and prof.get("valu_insts_per_launch"):
+            # MI355X_MICROARCH.md: a wave issues one VALU instruction per 2 cycles per SIMD
+            cap = 1024 * 2.4e9 / 2 * k_s
+            roof["valu"] = {"insts_per_launch": prof["valu_insts_per_launch"],
+                            "issue_frac": prof["valu_insts_per_launch"] / cap}
+        roof["note"] = ("the kernel's time is the longest history's dependent chain of popcount "
+                        "layers (VALU issue and LDS latency), see DESIGN.md §3.1")
     else:
-        roof.update({"config_bytes": st["config_bytes"], "grid_phases": st["phases"],
-                     "ret_steps": st["steps"], "candidates": st["candidates"],
+        roof.update({"grid_phases": st["phases"], "ret_steps": st["steps"],
                      "spill_inserts": st["spill_inserts"]})
 
     cpu = None
     parity = None
-    if not args.no_cpu and world == 1:
-        threads = min(16, os.cpu_count() or 1)
-        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, threads)
+    if not args.no_cpu and world == 1 and not args.emulate:
+        ci = cpu_info()
+        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, ci["threads"])
+        cpu.update({k: ci[k] for k in ("cpu_model", "nproc", "affinity")})
+        cpu["cores_from"] = ci["share"]
         if h.n_hist > 1:
             mism = [k for i, k in enumerate(sample)
                     if int(res["valid"][k]) != ores[i]["valid"] or
@@ -386,6 +477,10 @@ def main():
                       "mismatches": int(int(g["valid"][0]) != ores[0]["valid"] or
                                         int(g["explored"][0]) != ores[0]["explored"])}
 
+    desc = {"c1": "register 10 keys x 200 ops, 5 clients",
+            "c2": "register 1 key x 5k ops, 16 clients",
+            "c3": "jepsen.independent cas-register 1k keys x 1k ops, 5 clients/key",
+            "c4": "register 1 key x 100k ops, 16 clients, crashed :info ops"}[args.workload]
     out = {
         "metric": "history ops verified/sec (+ configs explored/sec, % HBM roofline)",
         "value": value,
@@ -395,27 +490,27 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (simulated linearizable SUT, SURVEY §8(d) seeds)",
-        "config": {"workload": f"{args.workload}: " + {
-            "c1": "register 10 keys x 200 ops, 5 clients",
-            "c2": "register 1 key x 5k ops, 16 clients",
-            "c3": "jepsen.independent cas-register 1k keys x 1k ops per GPU, 5 clients/key",
-            "c4": "register 1 key x 100k ops, 16 clients, crashed :info ops",
-            "c5": "counter 1M ops, 16 clients"}[args.workload],
-            "histories_per_gpu": h.n_hist, "ops_per_gpu": ops_rank, "p_info": cfg["p_info"],
-            "scale": args.scale, "parallelism": f"keys sharded over {world} GPU(s)"},
-        "configs_explored_per_s": total_cfg / elapsed,
+        "config": {"workload": f"{args.workload}: {desc}",
+                   "histories": h_all.n_hist, "ops": h_all.n_ops(), "p_info": cfg["p_info"],
+                   "scale": args.scale,
+                   "parallelism": f"keys split over {world} GPU(s) by LPT (lc_shard_histories)",
+                   "timed": "lc_plan_run: the search on encoded histories resident in HBM"},
+        "configs_explored_per_s": explored_all * args.steps / elapsed,
         "kernel_ms_per_step": kernel_ms / args.steps,
         "verdicts": vcount,
+        "end_to_end": e2e,
         "roofline": roof,
         "cpu_baseline": cpu,
         "parity_sample": parity,
     }
+    if args.emulate:
+        out["config"]["emulated"] = (f"rank {shard_rank} of {shard_world}: {h.n_hist} histories, "
+                                     f"{h.n_ops()} ops on this GPU; value counts them only")
     print(json.dumps(out), flush=True)
-    plan.close()
     if dist:
         dist[1].destroy_process_group()
 

@@ -5,7 +5,7 @@
  *   (checker/linearizable {:model (model/cas-register) :algorithm :linear})
  *       src/jepsen/jgroups/workload/register.clj:109-111 (inside independent/checker, :106)
  *   (checker/linearizable {:model (CounterModel. 0) :algorithm :linear})
- *       src/jepsen/jgroups/workload/counter.clj:135-137 (SURVEY numbering; file :250-254)
+ *       src/jepsen/jgroups/workload/counter.clj:133-137 (model CounterModel, :100-127)
  * Both construct a jepsen.checker/Checker whose (check test history opts) runs
  * knossos.linear/analysis [ext] and returns {:valid? ...}. A JVM caller binds these entry
  * points through JNA; Python binds them through ctypes (lincheck/_lib.py).
@@ -40,6 +40,7 @@ enum lc_error {
   LC_E_DEVICE = -2,    /* no usable HIP device / HIP runtime error */
   LC_E_MEMORY = -3,    /* device memory exhausted */
   LC_E_INTERNAL = -9,  /* kernel watchdog / internal consistency failure */
+  LC_E_CONFIGS = -10,  /* lc_failure_configs: the pre-failure frontier outgrew the dump capacity */
 };
 /* per-history error codes reported through out_err (valid == LC_UNKNOWN) */
 enum lc_hist_error {
@@ -62,8 +63,8 @@ int32_t lc_device_count(void);
  * Check n_hist histories against the model (knossos.linear semantics).
  *   model_kind   : LC_MODEL_CAS_REGISTER (initial value nil; init_value ignored) or
  *                  LC_MODEL_COUNTER (initial value init_value)
- *   n_gpus       : devices to spread histories over (<=0: all visible); results do not
- *                  depend on it
+ *   n_gpus       : shards to spread histories over (<=0: one per visible device; more
+ *                  shards than devices are multiplexed); results do not depend on it
  *   max_configs  : per-history cap on |frontier| + |closure| (<=0: device capacity only);
  *                  exceeding it reports LC_UNKNOWN with LC_H_CAPACITY (Knossos gives
  *                  :valid? :unknown when it runs out of memory [ext])
@@ -84,12 +85,22 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist,
                  char* err, int32_t err_len);
 
 /*
+ * The split lc_check uses for n_gpus > 1 (SURVEY §8(e) axis 1; jepsen.independent's per-key
+ * parallelism, register.clj:106): longest-processing-time over n_shards by entry count,
+ * out_shard[h] = shard of history h. Host-only (no device needed); deterministic. lc_check
+ * runs shard g on device g % (visible devices), so n_gpus may exceed the device count.
+ */
+int32_t lc_shard_histories(int32_t n_hist, const int64_t* hist_off, int32_t n_shards,
+                           int32_t* out_shard);
+
+/*
  * After lc_check reported history `hist` invalid: up to k configs of the frontier just
  * before the failing :ok (the :configs of a Knossos failure report [ext], compare as a
  * set). Config i: model value state[i] (register: nil when is_nil[i]), and the pending
  * ops it has linearized, as invocation :index values, in linearized[i*64 .. i*64+n_lin[i]).
  * The pending ops themselves (all of them) are written to pending[0..*n_pending).
- * Valid until the next lc_check on this thread.
+ * Valid until the next lc_check on this thread. Returns LC_E_CONFIGS when the frontier
+ * could not be dumped whole (the verdict stands; only the report is unavailable).
  */
 int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_nil,
                            int64_t* linearized, int32_t* n_lin, int32_t* n_out,
@@ -154,8 +165,12 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  * 14 dense big kernel ms (its own stream)               15 dense wave kernel ms (its own stream)
  * 16 dense big kernel algorithmic HBM bytes             17 dense big kernel algorithmic LDS bytes
  * 18 dense wave kernel algorithmic HBM bytes            19 dense wave kernel algorithmic LDS bytes
+ * 20..24 lc_plan_create phases, host wall ms: 20 encode (a4/a8), 21 first HIP call +
+ *    hipSetDevice, 22 streams/events/occupancy queries, 23 uploads, 24 dense step streams
+ * 25..27 dense big kernel: frontier configs in, frontier configs out, configs explored
+ * 28..30 the same for the dense wave (+ MID) kernel
  */
-#define LC_STATS_N 20
+#define LC_STATS_N 31
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
 void lc_plan_destroy(lc_plan* p);
 

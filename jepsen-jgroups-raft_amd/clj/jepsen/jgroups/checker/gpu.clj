@@ -1,77 +1,150 @@
 (ns jepsen.jgroups.checker.gpu
   "Drop-in for (checker/linearizable {:model m :algorithm :linear}) backed by
   liblincheck.so (include/lincheck.h) through JNA. Reference call sites replaced:
-  src/jepsen/jgroups/workload/register.clj:109-111 and counter.clj:135-137 (SURVEY
-  numbering; file lines :250-254). Not executable in the build container (no JVM):
-  the Python ctypes harness (lincheck/_lib.py) makes the same calls with the same
-  arrays and is what the tests exercise."
+  src/jepsen/jgroups/workload/register.clj:106-111 (independent/checker over
+  checker/linearizable) and counter.clj:133-137 (model CounterModel, :100-127).
+
+  UNTESTED ON A JVM: the build container and the GPU box have no JVM, so this file has
+  never been loaded. The Python ctypes harness (lincheck/_lib.py, lincheck/checker.py)
+  makes the same calls with the same arrays and is what the tests exercise."
   (:require [jepsen.checker :as checker]
             [jepsen.independent :as independent]
             [knossos.model :as model])
-  (:import (com.sun.jna Native NativeLibrary Function Memory)
+  (:import (com.sun.jna NativeLibrary Function)
            (knossos.model CASRegister)))
 
 (def ^:private lib (delay (NativeLibrary/getInstance "lincheck")))
 
-(defn- f [name] (.getFunction ^NativeLibrary @lib name))
+(defn- lib-fn
+  "The exported C function `fname` of liblincheck.so."
+  ^Function [fname]
+  (.getFunction ^NativeLibrary @lib ^String fname))
 
 (def type-code {:invoke 0 :ok 1 :fail 2 :info 3})
 (def f-code {:read 0 :write 1 :cas 2 :add 3 :decr 4 :add-and-get 5 :decr-and-get 6})
 
+(def ^:private err-text
+  {-4 "malformed history" -5 "too many concurrently pending ops"
+   -6 "model cannot step an op" -7 "frontier exceeded max-configs / device capacity"})
+
+(defn- c-string [^bytes buf]
+  (String. buf 0 (int (or (first (keep-indexed #(when (zero? %2) %1) buf)) (alength buf)))))
+
 (defn- encode
   "Histories (seq of op vectors) -> SoA primitive arrays in lincheck.h order."
   [histories]
-  (let [ops   (vec (apply concat histories))
-        n     (count ops)
-        off   (long-array (reductions + 0 (map count histories)))
-        index (long-array n) process (int-array n) type (byte-array n) fs (byte-array n)
-        v0 (long-array n) v1 (long-array n) vflags (byte-array n)]
+  (let [ops    (vec (apply concat histories))
+        n      (count ops)
+        off    (long-array (reductions + 0 (map count histories)))
+        index  (long-array n) process (int-array n) types (byte-array n) fs (byte-array n)
+        v0     (long-array n) v1 (long-array n) vflags (byte-array n)]
     (dotimes [i n]
       (let [op (nth ops i) v (:value op)]
         (aset index i (long (:index op i)))
         (aset process i (int (:process op)))
-        (aset type i (byte (type-code (:type op))))
+        (aset types i (byte (type-code (:type op))))
         (aset fs i (byte (f-code (:f op))))
         (cond (nil? v)    (aset vflags i (byte 0))
-              (vector? v) (do (aset vflags i (byte 2)) (aset v0 i (long (v 0))) (aset v1 i (long (v 1))))
+              (vector? v) (do (aset vflags i (byte 2))
+                              (aset v0 i (long (v 0)))
+                              (aset v1 i (long (v 1))))
               :else       (do (aset vflags i (byte 1)) (aset v0 i (long v))))))
-    {:off off :index index :process process :type type :f fs :v0 v0 :v1 v1 :vflags vflags}))
+    {:off off :index index :process process :types types :fs fs :v0 v0 :v1 v1 :vflags vflags}))
+
+(defn- failure-configs
+  "lc_failure_configs for history i of the lc_check this thread just made: up to k
+  pre-failure configs as {:model {:value v} :linearized [inv-index ...] :pending [...]},
+  or nil when the frontier could not be dumped (the verdict stands)."
+  [i k]
+  (let [state (long-array k) nils (byte-array k) lin (long-array (* 64 k)) n-lin (int-array k)
+        n-out (int-array 1) pending (long-array 64) n-pending (int-array 1) err (byte-array 512)
+        rc (.invokeInt (lib-fn "lc_failure_configs")
+                       (object-array [(int i) (int k) state nils lin n-lin n-out pending n-pending
+                                      err (int 512)]))]
+    (when (zero? rc)
+      (let [pend (vec (take (aget n-pending 0) pending))]
+        (vec (for [c (range (aget n-out 0))]
+               {:model      {:value (when (zero? (aget nils c)) (aget state c))}
+                :linearized (vec (for [x (range (aget n-lin c))] (aget lin (+ (* 64 c) x))))
+                :pending    pend}))))))
 
 (defn check-histories
   "One lc_check call for many histories; returns a vector of Knossos-keyed maps."
   [model-kind init histories opts]
-  (let [{:keys [off index process type f v0 v1 vflags]} (encode histories)
-        k (count histories)
-        valid (byte-array k) fail (long-array k) finv (long-array k) prev (long-array k)
+  (let [{:keys [off index process types fs v0 v1 vflags]} (encode histories)
+        k        (count histories)
+        valid    (byte-array k) fail (long-array k) finv (long-array k) prev (long-array k)
         explored (long-array k) errs (int-array k) err (byte-array 512)
-        rc (.invokeInt ^Function (f "lc_check")
-                       (object-array [(int model-kind) (long init) (int k) off index process type
-                                      f v0 v1 vflags (int (:gpus opts 0)) (long (:max-configs opts 0))
-                                      (int 0) valid fail finv prev explored errs err (int 512)]))]
+        rc       (.invokeInt (lib-fn "lc_check")
+                             (object-array [(int model-kind) (long init) (int k) off index process
+                                            types fs v0 v1 vflags (int (:gpus opts 0))
+                                            (long (:max-configs opts 0)) (int 0) valid fail finv
+                                            prev explored errs err (int 512)]))]
     (when-not (zero? rc)
-      (throw (ex-info (String. err 0 (int (or (first (keep-indexed #(when (zero? %2) %1) err)) 512)))
-                      {:rc rc})))
+      (throw (ex-info (c-string err) {:rc rc})))
     (vec (for [i (range k)]
            (let [ops (nth histories i)
-                 at  (fn [idx] (first (filter #(= idx (:index %)) ops)))]
-             (cond-> {:valid?   (case (aget valid i) 1 true 0 false :unknown)
+                 at  (fn [idx] (first (filter #(= idx (:index %)) ops)))
+                 v   (aget valid i)]
+             (cond-> {:valid?   (case v 1 true 0 false :unknown)
                       :analyzer :linear
                       :explored (aget explored i)}
-               (zero? (aget valid i)) (assoc :op (at (aget fail i))
-                                             :previous-ok (at (aget prev i))
-                                             :last-op (at (aget prev i)))))))))
+               (= 2 v)    (assoc :error (get err-text (aget errs i) "undecided"))
+               (zero? v)  (assoc :op          (at (aget fail i))
+                                 :previous-ok (at (aget prev i))
+                                 ;; the op linearized last before the failure: JIT
+                                 ;; linearization returns the previous :ok op last
+                                 :last-op     (at (aget prev i)))
+               (and (zero? v) (:configs opts true))
+               (assoc :configs (failure-configs i 10))))))))
 
-(defn- model-kind [m]
-  (cond (instance? CASRegister m) [1 0]
-        (= "CounterModel" (.getSimpleName (class m))) [2 (long (:value m))]
+(defn- model-kind
+  "[model_kind init] for the models the GPU implements, else nil (-> Knossos)."
+  [m]
+  (cond (and (instance? CASRegister m) (nil? (:value m))) [1 0]  ; (model/cas-register)
+        (= "CounterModel" (.getSimpleName (class m)))       [2 (long (:value m))]
         :else nil))
 
+(defn- client-ops [history] (filterv #(integer? (:process %)) history))
+
 (defn linearizable
-  "Same options as checker/linearizable. Models the GPU does not implement (e.g. the
-  election workload's LeaderModel, leader.clj:63-75) fall back to Knossos."
+  "Same options as checker/linearizable. Models the GPU does not implement (the election
+  workload's LeaderModel, leader.clj:63-85; a cas-register with a non-nil initial value)
+  fall back to Knossos."
   [{:keys [model] :as opts}]
   (if-let [[kind init] (model-kind model)]
     (reify checker/Checker
       (check [_ test history copts]
-        (first (check-histories kind init [(filterv #(integer? (:process %)) history)] opts))))
+        (first (check-histories kind init [(client-ops history)] opts))))
     (checker/linearizable opts)))
+
+(defn independent-checker
+  "Batched drop-in for register.clj:106-111,
+    (independent/checker (checker/compose {:timeline (timeline/html)
+                                           :linear (checker/linearizable opts)}))
+  Splits the history by key (jepsen.independent/history-keys, subhistory), sends EVERY key
+  down in one lc_check, runs the other per-key checkers (e.g. {:timeline (timeline/html)})
+  as compose would, and returns {:valid? :results {k {:linear .. :timeline ..}} :failures}.
+  Falls back to the per-key independent/checker when the model is not a GPU model."
+  ([opts] (independent-checker opts {}))
+  ([{:keys [model] :as opts} others]
+   (if-let [[kind init] (model-kind model)]
+     (reify checker/Checker
+       (check [_ test history copts]
+         (let [ks      (vec (independent/history-keys history))
+               subs    (mapv #(client-ops (independent/subhistory % history)) ks)
+               linears (if (seq ks) (check-histories kind init subs opts) [])
+               results (into {}
+                             (map (fn [k sub lin]
+                                    (let [kopts (assoc copts :subdirectory ["independent" k]
+                                                             :history-key k)
+                                          r     (into {:linear lin}
+                                                      (for [[n c] others]
+                                                        [n (checker/check-safe c test sub kopts)]))]
+                                      [k (assoc r :valid? (checker/merge-valid (map :valid? (vals r))))]))
+                                  ks subs linears))]
+           {:valid?   (checker/merge-valid (map :valid? (vals results)))
+            :results  results
+            ;; jepsen.independent: keys whose :valid? is falsey (:unknown is truthy)
+            :failures (vec (for [[k r] results :when (false? (:valid? r))] k))})))
+     (independent/checker (checker/compose (assoc others :linear (checker/linearizable opts)))))))

@@ -151,6 +151,9 @@ struct lc_plan {
   std::vector<int32_t> status, fail_step;
   std::vector<unsigned long long> explored;
   double stats[LC_STATS_N] = {0};
+  // lc_plan_create phases (ms): encode, hipSetDevice (+ runtime init), streams/events/occupancy,
+  // uploads, build_dense (reported as stats 20..24)
+  double phase_ms[5] = {0};
   int32_t max_t = INT32_MAX;  // failure-frontier dump mode (grid kernel)
   int64_t entry_bytes() const { return model == LC_MODEL_CAS_REGISTER ? 8 : 16; }
   int state_bits_of(int h) const {
@@ -211,7 +214,14 @@ struct lc_plan {
   }
 
   int init_device() {
+    auto t0 = std::chrono::steady_clock::now();
+    auto ms_since = [](std::chrono::steady_clock::time_point t) {
+      return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipFree(nullptr));  // forces runtime/context initialisation into this phase
+    phase_ms[1] = ms_since(t0);
+    t0 = std::chrono::steady_clock::now();
     if (!stream) HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     if (!ev0) HIP_TRY(hipEventCreate(&ev0));
     if (!ev1) HIP_TRY(hipEventCreate(&ev1));
@@ -249,6 +259,7 @@ struct lc_plan {
     // test hooks: tiny cells / overflow buckets exercise the overflow and regrow paths
     if ((e = getenv("LC_CELLCAP")) && atoi(e) > 0) cell_cap = atoi(e);
     if ((e = getenv("LC_OVFCAP")) && atoll(e) > 0) ovf_cap = atoll(e);
+    phase_ms[2] = ms_since(t0);
     return 0;
   }
 
@@ -285,7 +296,10 @@ struct lc_plan {
     if ((rc = upload(d_kbits, kbi))) return rc;
     if ((rc = upload(d_order, order))) return rc;
     HIP_TRY(d_queue.ensure(8));
-    return build_dense();
+    auto t0 = std::chrono::steady_clock::now();
+    rc = build_dense();
+    phase_ms[4] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
   }
 
   // Algorithmic bytes of one dense step with live slots `live` and ninv invocations
@@ -395,9 +409,10 @@ struct lc_plan {
     const int nm = (int)dense_m.size();
     if (nb + nw + nx + nm == 0) return 0;
     const int n = enc.n_hist;
-    HIP_TRY(d_stats.ensure(SS_N * 8));
+    // one stats block per kernel: big, wave, MID
+    HIP_TRY(d_stats.ensure(3 * SS_N * 8));
     HIP_TRY(hipMemsetAsync(d_dqueue.p, 0, 16, stream));
-    HIP_TRY(hipMemsetAsync(d_stats.p, 0, SS_N * 8, stream));
+    HIP_TRY(hipMemsetAsync(d_stats.p, 0, 3 * SS_N * 8, stream));
     HIP_TRY(hipMemsetAsync(d_dexpl.p, 0, (size_t)std::max(n, 1) * 8, stream));
     DenseParams p{};
     p.sbeg = d_dsbeg.as<int64_t>();
@@ -508,6 +523,7 @@ struct lc_plan {
       q.n = nw;
       q.order = d_dorder.as<int32_t>() + nb;
       q.queue = d_dqueue.as<int32_t>() + 1;
+      q.stats = d_stats.as<unsigned long long>() + SS_N;
       HIP_TRY(hipEventRecord(ev_w0, stream2));
       HIP_TRY(launch_dense(q, DENSE_WAVE, std::min(dgrid_w, (nw + 3) / 4), stream2));
       HIP_TRY(hipEventRecord(ev_w1, stream2));
@@ -520,6 +536,7 @@ struct lc_plan {
       q.n = nm;
       q.order = d_dorder.as<int32_t>() + nb + nw + nx;
       q.queue = d_dqueue.as<int32_t>() + 2;
+      q.stats = d_stats.as<unsigned long long>() + 2 * SS_N;
       HIP_TRY(hipEventRecord(ev_m0, stream3));
       // wave + MID workgroups stay within one per CU: either fits beside a big-kernel
       // workgroup, two of them do not, and every tile-team workgroup must be resident
@@ -593,8 +610,9 @@ struct lc_plan {
     HIP_TRY(hipMemcpy(st.data(), d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(fs.data(), d_dfail.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(ex.data(), d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost));
-    unsigned long long ss[SS_N];
-    HIP_TRY(hipMemcpy(ss, d_stats.p, sizeof(ss), hipMemcpyDeviceToHost));
+    unsigned long long ss3[3 * SS_N], ss[SS_N];
+    HIP_TRY(hipMemcpy(ss3, d_stats.p, sizeof(ss3), hipMemcpyDeviceToHost));
+    for (int i = 0; i < SS_N; ++i) ss[i] = ss3[i] + ss3[SS_N + i] + ss3[2 * SS_N + i];
     for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
       for (int h : *ids) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
     stats[1] += (nw ? 1 : 0) + (nm ? 1 : 0) + (double)launches.size();
@@ -619,6 +637,20 @@ struct lc_plan {
     stats[2] += (double)ss[SS_STEPS];
     stats[4] += (double)ss[SS_FOUT] + (nb + nw + nx + nm);  // frontier in = previous frontier out (+ initial)
     stats[6] += (double)ss[SS_FOUT];
+    // per kernel (SURVEY §8(d) terms): 25..27 big F_in / F_out / explored, 28..30 wave (+MID);
+    // a history's frontier out of every step but its last is the next step's frontier in
+    {
+      double ex_big = 0, ex_wave = 0;
+      for (const std::vector<int>* ids : {&dense_b, &dense_x}) for (int h : *ids) ex_big += (double)ex[h];
+      for (const std::vector<int>* ids : {&dense_w, &dense_m}) for (int h : *ids) ex_wave += (double)ex[h];
+      const double fo_big = (double)ss3[SS_FOUT], fo_wave = (double)(ss3[SS_N + SS_FOUT] + ss3[2 * SS_N + SS_FOUT]);
+      stats[25] += fo_big + (nb + nx);
+      stats[26] += fo_big;
+      stats[27] += ex_big;
+      stats[28] += fo_wave + (nw + nm);
+      stats[29] += fo_wave;
+      stats[30] += ex_wave;
+    }
     if (debug()) {
       fprintf(stderr, "[lincheck] dense: %d block + %d wave + %d tile-team histories (%zu launch(es), %zu team "
               "workgroups): %.3f ms, steps=%llu Fout=%llu\n", nb, nw, nx, launches.size(), max_wgs, t,
@@ -1007,6 +1039,7 @@ struct lc_plan {
     fail_step.assign(enc.n_hist, -1);
     explored.assign(enc.n_hist, 0);
     std::fill(stats, stats + LC_STATS_N, 0.0);
+    for (int i = 0; i < 5; ++i) stats[20 + i] = phase_ms[i];
     float ms = 0;
     int rc = 0;
     std::vector<int> grid_ids;
@@ -1080,13 +1113,25 @@ namespace {
 
 int plan_build(int device, int model, int64_t init_value, int n_hist, const int64_t* hist_off,
                const HistArrays& a, int64_t max_configs, lc_plan** out, std::string& msg) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) {
+    return std::chrono::duration<double, std::milli>(clk::now() - t).count();
+  };
   auto p = std::make_unique<lc_plan>();
   p->device = device;
   p->model = model;
   p->max_configs = max_configs;
+  auto t = clk::now();
   encode(model, init_value, n_hist, hist_off, a, p->enc);
-  int rc = p->init_device();
-  if (!rc) rc = p->upload_encoded();
+  p->phase_ms[0] = ms_since(t);
+  int rc = p->init_device();  // records phase_ms[1] (hipSetDevice) and [2] (streams, occupancy)
+  t = clk::now();
+  if (!rc) rc = p->upload_encoded();  // records phase_ms[4] (build_dense)
+  p->phase_ms[3] = ms_since(t) - p->phase_ms[4];
+  if (debug() || getenv("LC_PHASES"))
+    fprintf(stderr, "[lincheck] plan_create phases (ms): encode %.2f  hipSetDevice %.2f  streams+occupancy %.2f  "
+            "uploads %.2f  build_dense %.2f\n", p->phase_ms[0], p->phase_ms[1], p->phase_ms[2], p->phase_ms[3],
+            p->phase_ms[4]);
   if (rc) {
     msg = p->last_error;
     return rc;
@@ -1116,6 +1161,21 @@ bool valid_args(int model, int n_hist, const int64_t* hist_off, const int32_t* p
     return false;
   }
   return true;
+}
+
+// Longest-processing-time split of histories over G shards by entry count: heaviest first,
+// each to the least-loaded shard (lowest index on ties); deterministic. Host only.
+void lpt_shards(int n_hist, const int64_t* off, int G, int32_t* out_shard) {
+  std::vector<int> order(n_hist);
+  for (int h = 0; h < n_hist; ++h) order[h] = h;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int x, int y) { return off[x + 1] - off[x] > off[y + 1] - off[y]; });
+  std::vector<int64_t> load(G, 0);
+  for (int h : order) {
+    const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    out_shard[h] = g;
+    load[g] += off[h + 1] - off[h];
+  }
 }
 
 // state of the most recent lc_check on this thread (for lc_failure_configs)
@@ -1151,15 +1211,20 @@ int32_t lc_plan_create(int32_t device, int32_t model_kind, int64_t init_value, i
   *out = nullptr;
   if (!valid_args(model_kind, n_hist, hist_off, process, type, f, v0, v1, vflags, err, err_len))
     return LC_E_ARG;
+  const auto t0 = std::chrono::steady_clock::now();
+  // the first HIP call of the process initialises the runtime: counted with hipSetDevice
   if (lc_device_count() <= device || device < 0) {
     set_err(err, err_len, "no HIP device %d (the checker has no CPU fallback)", device);
     return LC_E_DEVICE;
   }
+  const double count_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::lock_guard<std::mutex> g(device_mutex(device));
   HistArrays a{hist_off[n_hist] - hist_off[0], index, process, type, f, v0, v1, vflags};
   std::string msg;
   int rc = plan_build(device, model_kind, init_value, n_hist, hist_off, a, max_configs, out, msg);
   if (rc) set_err(err, err_len, "%s", msg.c_str());
+  else (*out)->phase_ms[1] += count_ms;
   return rc;
 }
 
@@ -1204,7 +1269,9 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
     set_err(err, err_len, "no HIP device visible (the checker has no CPU fallback)");
     return LC_E_DEVICE;
   }
-  int G = n_gpus <= 0 ? ndev : std::min(n_gpus, ndev);
+  // shards: one per requested GPU; more shards than visible devices are multiplexed over
+  // them (shard g on device g % ndev, serialised by the device mutex; results do not change)
+  int G = n_gpus <= 0 ? ndev : n_gpus;
   G = std::max(1, std::min(G, std::max(1, n_hist)));
 
   // keep a copy for lc_failure_configs
@@ -1255,18 +1322,9 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
   // shard histories over devices: longest-processing-time on entry counts
   std::vector<std::vector<int>> shard(G);
   {
-    std::vector<int> order(n_hist);
-    for (int h = 0; h < n_hist; ++h) order[h] = h;
-    std::sort(order.begin(), order.end(), [&](int x, int y) {
-      return L.off[x + 1] - L.off[x] > L.off[y + 1] - L.off[y];
-    });
-    std::vector<int64_t> load(G, 0);
-    for (int h : order) {
-      int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-      shard[g].push_back(h);
-      load[g] += L.off[h + 1] - L.off[h];
-    }
-    for (auto& s : shard) std::sort(s.begin(), s.end());
+    std::vector<int32_t> of(n_hist);
+    lpt_shards(n_hist, L.off.data(), G, of.data());
+    for (int h = 0; h < n_hist; ++h) shard[of[h]].push_back(h);
   }
   std::vector<int> rcs(G, 0);
   std::vector<std::string> msgs(G);
@@ -1289,10 +1347,11 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
       }
       off.push_back((int64_t)idx.size());
     }
-    std::lock_guard<std::mutex> lk(device_mutex(g));
+    const int dev = g % ndev;
+    std::lock_guard<std::mutex> lk(device_mutex(dev));
     HistArrays a{off.back(), idx.data(), pr.data(), ty.data(), ff.data(), a0.data(), a1.data(), vf.data()};
     lc_plan* p = nullptr;
-    int rc = plan_build(g, model_kind, init_value, (int)hs.size(), off.data(), a, max_configs, &p, msgs[g]);
+    int rc = plan_build(dev, model_kind, init_value, (int)hs.size(), off.data(), a, max_configs, &p, msgs[g]);
     if (!rc) {
       rc = p->run();
       if (rc) msgs[g] = p->last_error;
@@ -1311,11 +1370,10 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
         if (out_prev_ok) out_prev_ok[h] = po[k];
         if (out_explored) out_explored[h] = ex[k];
         if (out_err) out_err[h] = er[k];
-        g_last.valid.resize(n_hist);
       }
     }
     if (p) {
-      hipSetDevice(g);
+      hipSetDevice(dev);
       delete p;
     }
     rcs[g] = rc;
@@ -1329,10 +1387,19 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
   }
   for (int g = 0; g < G; ++g)
     if (rcs[g]) {
-      set_err(err, err_len, "device %d: %s", g, msgs[g].c_str());
+      set_err(err, err_len, "shard %d (device %d): %s", g, g % ndev, msgs[g].c_str());
       return rcs[g];
     }
+  if (out_valid) g_last.valid.assign(out_valid, out_valid + n_hist);
   g_last.have = true;
+  return 0;
+}
+
+int32_t lc_shard_histories(int32_t n_hist, const int64_t* hist_off, int32_t n_shards, int32_t* out_shard) {
+  if (n_hist < 0 || n_shards < 1 || (n_hist > 0 && (!hist_off || !out_shard))) return LC_E_ARG;
+  for (int h = 0; h < n_hist; ++h)
+    if (hist_off[h + 1] < hist_off[h]) return LC_E_ARG;
+  lpt_shards(n_hist, hist_off, n_shards, out_shard);
   return 0;
 }
 
@@ -1368,10 +1435,17 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
   }
   const int t_fail = p->fail_step[0];
   p->max_t = t_fail;  // stop before the failing RETURN: the frontier it saw stays in flist
-  rc = p->run();
+  rc = p->run();      // (the grid kernel: the dense tables keep no config lists)
   if (rc) {
     set_err(err, err_len, "%s", p->last_error.c_str());
     return rc;
+  }
+  if (p->status[0] != ST_RUNNING) {
+    // the grid kernel's frontier lists overflowed before step t_fail (the verdict itself may
+    // have come from the dense tables, which have no such limit): the lists are partial
+    set_err(err, err_len, "failure configs unavailable: the pre-failure frontier of history %d exceeds the "
+            "grid kernel's capacity (status %d)", hist, p->status[0]);
+    return LC_E_CONFIGS;
   }
   // replay slot assignments to step t_fail
   const Encoded& en = p->enc;

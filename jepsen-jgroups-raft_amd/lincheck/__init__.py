@@ -3,7 +3,7 @@ checker/linearizable {:algorithm :linear} on cas-register and CounterModel histo
 from . import history, model
 from .checker import (Checker, check_safe, compose, independent_checker, linearizable,
                       merge_valid, timeline_html)
-from .model import CounterModel, cas_register
+from .model import CounterModel, LeaderModel, cas_register
 
 __all__ = ["history", "model", "Checker", "check_safe", "compose", "independent_checker",
-           "linearizable", "merge_valid", "timeline_html", "CounterModel", "cas_register"]
+           "linearizable", "merge_valid", "timeline_html", "CounterModel", "LeaderModel", "cas_register"]

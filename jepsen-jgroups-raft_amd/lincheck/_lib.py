@@ -12,18 +12,22 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liblincheck.so")
 
 # every symbol include/lincheck.h declares (tests check the exports)
-EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_failure_configs",
+EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_shard_histories",
+           "lc_failure_configs",
            "lc_counter_bounds", "lc_plan_create", "lc_plan_run", "lc_plan_results",
            "lc_plan_stats", "lc_plan_destroy", "lc_bounds_plan_create", "lc_bounds_plan_sums",
            "lc_bounds_plan_run", "lc_bounds_plan_destroy", "lc_part_create", "lc_part_info",
            "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
            "lc_part_step_end", "lc_part_results", "lc_part_destroy")
-STATS_N = 20
+STATS_N = 31
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
                "spill_inserts", "dense_histories", "dense_ms", "dense_big_ms", "dense_wave_ms",
                "dense_big_hbm_bytes", "dense_big_lds_bytes", "dense_wave_hbm_bytes",
-               "dense_wave_lds_bytes")
+               "dense_wave_lds_bytes", "create_encode_ms", "create_device_init_ms",
+               "create_streams_ms", "create_upload_ms", "create_dense_streams_ms",
+               "dense_big_frontier_in", "dense_big_frontier_out", "dense_big_explored",
+               "dense_wave_frontier_in", "dense_wave_frontier_out", "dense_wave_explored")
 
 P = C.c_void_p
 I8P = C.POINTER(C.c_int8)
@@ -47,6 +51,8 @@ def load():
     L.lc_check.argtypes = [C.c_int32, C.c_int64, C.c_int32] + [P] * 8 + \
         [C.c_int32, C.c_int64, C.c_int32] + [P] * 6 + [C.c_char_p, C.c_int32]
     L.lc_check.restype = C.c_int32
+    L.lc_shard_histories.argtypes = [C.c_int32, P, C.c_int32, P]
+    L.lc_shard_histories.restype = C.c_int32
     L.lc_failure_configs.argtypes = [C.c_int32, C.c_int32] + [P] * 7 + [C.c_char_p, C.c_int32]
     L.lc_failure_configs.restype = C.c_int32
     L.lc_counter_bounds.argtypes = [C.c_int64, C.c_int32] + [P] * 10 + [C.c_char_p, C.c_int32]
@@ -127,6 +133,15 @@ def check(model_kind: int, init_value: int, h, n_gpus: int = 1, max_configs: int
                     _p(out["explored"]), _p(out["err"]), buf, len(buf))
     _raise(rc, buf, "lc_check")
     return out
+
+
+def shard_histories(h, n_shards: int) -> np.ndarray:
+    """lc_shard_histories: the LPT split lc_check uses over n_shards (host only)."""
+    out = np.zeros(max(h.n_hist, 1), np.int32)
+    rc = load().lc_shard_histories(h.n_hist, _p(h.off), n_shards, _p(out))
+    if rc != 0:
+        raise LincheckError(f"lc_shard_histories failed ({rc})")
+    return out[:h.n_hist]
 
 
 def failure_configs(hist: int, k: int = 10):

@@ -3,8 +3,8 @@
 Mirrors the op shapes the reference's clients produce:
   * register: read invoke value nil, ok value long-or-nil (register.clj:16-19, :74-75);
     write keeps its value (:77-78); cas ok -> [old new] (:83); cas failure -> :fail (:84)
-  * counter: read ok -> long (counter.clj:82-83 in SURVEY numbering, here :199-200);
-    add/decr keep the delta; *-and-get ok -> [delta result] (:208-210)
+  * counter: read ok -> long (counter.clj:82-83);
+    add/decr keep the delta; *-and-get ok -> [delta result] (:91-93)
   * independent keys: value = (tuple k v) (jepsen.independent [ext]; register.clj:75, :83)
   * error classification (client.clj:52-63): timeouts of non-idempotent ops -> :info
 

@@ -38,13 +38,17 @@ class _Exchange:
         self.cdev = device if self.nccl else "cpu"  # where collective tensors live
         self.bytes = 0
 
-    def gather_counts(self, counts: np.ndarray) -> np.ndarray:
+    def gather_counts(self, counts: np.ndarray, over: bool):
+        """All-gather every rank's per-destination counts plus its capacity flag ->
+        ([src][dst] counts, whether any rank overflowed)."""
         import torch
-        mine = torch.as_tensor(counts, dtype=torch.int64).to(self.cdev)
-        allv = torch.empty(self.world * self.world, dtype=torch.int64, device=self.cdev)
+        w = self.world + 1
+        mine = torch.as_tensor(np.append(counts, int(over)), dtype=torch.int64).to(self.cdev)
+        allv = torch.empty(self.world * w, dtype=torch.int64, device=self.cdev)
         self.tdist.all_gather_into_tensor(allv, mine) if self.nccl else \
-            self.tdist.all_gather(list(allv.view(self.world, self.world).unbind(0)), mine)
-        return allv.view(self.world, self.world).cpu().numpy()  # [src][dst]
+            self.tdist.all_gather(list(allv.view(self.world, w).unbind(0)), mine)
+        a = allv.view(self.world, w).cpu().numpy()
+        return a[:, :self.world], bool(a[:, self.world].any())
 
     def all_to_all(self, send, n_send: int, in_splits, out_splits, recv_pool):
         """send[:n_send] (device tensor, by destination) -> received device tensor."""
@@ -62,11 +66,12 @@ class _Exchange:
         self.bytes += 8 * (n_send + n_recv)
         return recv, n_recv
 
-    def sum(self, v: int) -> int:
+    def sum(self, v: int, over: bool = False):
+        """All-reduce SUM of v and of the capacity flags -> (sum, whether any rank overflowed)."""
         import torch
-        t = torch.tensor([int(v)], dtype=torch.int64, device=self.cdev)
+        t = torch.tensor([int(v), int(over)], dtype=torch.int64, device=self.cdev)
         self.tdist.all_reduce(t)
-        return int(t.item())
+        return int(t[0].item()), bool(t[1].item())
 
 
 def search(plan, tdist=None, device="cpu", stream=None, max_steps=None):
@@ -94,38 +99,63 @@ def search(plan, tdist=None, device="cpu", stream=None, max_steps=None):
         return {"valid": 2, "fail_step": -1, "fail_idx": -1, "fail_inv": -1, "prev_ok": -1,
                 "explored": 0, "err": plan.err, "steps": 0, "levels": 0, "exchanged_bytes": 0,
                 "wall_s": 0.0}
+    # Capacity is per rank (this rank's hash sets and lists). A rank that overflows stops
+    # calling its plan but keeps taking part in the level's collectives with empty sends; its
+    # flag rides on the next count all-gather or frontier all-reduce, so every rank leaves at
+    # the same collective and reports :unknown together (no mismatched collectives).
+    over = False
+
+    def attempt(fn, *a):
+        nonlocal over
+        if over:
+            return None
+        try:
+            return fn(*a)
+        except _lib.CapacityError:
+            over = True
+            return None
+
     t = -1
-    try:
-        for t in range(n_steps):
-            plan.step_begin(t, stream)
-            while True:
-                counts = plan.expand(stream)
-                levels += 1
-                if world == 1:
-                    n = int(counts[0])
-                    if n == 0:
-                        break
-                    plan.absorb(None, n, stream)
-                    continue
-                cm = ex.gather_counts(counts)
-                if int(cm.sum()) == 0:
+    any_over = False
+    for t in range(n_steps):
+        attempt(plan.step_begin, t, stream)
+        while True:
+            counts = attempt(plan.expand, stream)
+            if counts is None:
+                counts = np.zeros(world, np.int64)
+            levels += 1
+            if world == 1:
+                any_over = over
+                n = int(counts[0])
+                if n == 0 or over:
                     break
-                n_send = int(counts.sum())
-                send = buf("send", n_send)
-                plan.pack(send, stream)
-                recv, n_recv = ex.all_to_all(send, n_send, counts.tolist(), cm[:, rank].tolist(),
-                                             lambda n: buf("recv", n))
-                plan.absorb(recv, n_recv, stream)
-            mine = plan.step_end(stream)
-            total = mine if world == 1 else ex.sum(mine)
-            if total == 0:
-                fail_t = t
-                valid = 0
+                attempt(plan.absorb, None, n, stream)
+                continue
+            cm, any_over = ex.gather_counts(counts, over)
+            if any_over or int(cm.sum()) == 0:
                 break
-    except _lib.CapacityError:
+            n_send = int(counts.sum())
+            send = buf("send", n_send)
+            attempt(plan.pack, send, stream)
+            recv, n_recv = ex.all_to_all(send, n_send, counts.tolist(), cm[:, rank].tolist(),
+                                         lambda n: buf("recv", n))
+            attempt(plan.absorb, recv, n_recv, stream)
+        if any_over:
+            break
+        mine = attempt(plan.step_end, stream)
+        mine = 0 if mine is None else mine
+        total, any_over = (mine, over) if world == 1 else ex.sum(mine, over)
+        if any_over:
+            break
+        if total == 0:
+            fail_t = t
+            valid = 0
+            break
+    if any_over:
         valid, err = 2, _lib.PartPlan.H_CAPACITY
-    expl, fidx, finv, prev = plan.results(fail_t if fail_t >= 0 else t, stream)
-    explored = expl if world == 1 else ex.sum(expl)
+    res = attempt(plan.results, fail_t if fail_t >= 0 else t, stream) or (0, -1, -1, -1)
+    expl, fidx, finv, prev = res
+    explored = expl if world == 1 else ex.sum(expl)[0]
     st = plan.stats() if hasattr(plan, "stats") else {"kernel_ms": 0.0, "alg_bytes": 0.0}
     return {"valid": valid, "fail_step": fail_t,
             "fail_idx": fidx if valid == 0 else -1, "fail_inv": finv if valid == 0 else -1,

@@ -9,7 +9,7 @@ Reads the history with lincheck.edn and runs the same checker the reference's wo
           {:model (model/cas-register) :algorithm :linear})}))           register.clj:106-111
   counter:
       (checker/compose {:timeline .. :linear (checker/linearizable
-          {:model (CounterModel. 0) :algorithm :linear})})                counter.clj:250-254
+          {:model (CounterModel. 0) :algorithm :linear})})                counter.clj:133-137
 and prints the result map as JSON (keywords as strings, ops as maps).
 """
 from __future__ import annotations

@@ -9,8 +9,8 @@ Value domains follow the reference generators:
   * register: f mix 1/3 read/write/cas (register.clj:116), values U{0..4} (:21-34);
     a cas whose expected value does not match is a definite :fail (:84); CAS on a nil
     register fails (ReplicatedMap.java:37-48).
-  * counter: f uniform over read/add/decr/add-and-get/decr-and-get (counter.clj:255),
-    deltas U{0..4} (:132-155); *-and-get ok -> [delta new] (:208-210).
+  * counter: f uniform over read/add/decr/add-and-get/decr-and-get (counter.clj:138),
+    deltas U{0..4} (:15-38); *-and-get ok -> [delta new] (:91-93).
 Error model (client.clj:52-63): with probability p_info a non-read op times out ->
 :info (applied with probability 1/2, possibly after its completion time) and the client
 continues under a fresh process id (p + n_clients); a timed-out read is :fail.

@@ -82,8 +82,9 @@ def encode_register(h, hist=0):
 class MockPartPlan:
     H_CAPACITY = -7
 
-    def __init__(self, h, hist=0, rank=0, world=1):
+    def __init__(self, h, hist=0, rank=0, world=1, set_cap=None):
         self.rank, self.world = rank, world
+        self.set_cap = set_cap  # capacity of this rank's closure set (None: unbounded)
         self.steps, self.mask_bits = encode_register(h, hist)
         self.n_steps = len(self.steps)
         self.err = 0
@@ -141,6 +142,9 @@ class MockPartPlan:
                     self.O.add(o)
                     self.OUT.append(o)
             elif key not in self.S:
+                if self.set_cap is not None and len(self.S) >= self.set_cap:
+                    from lincheck._lib import CapacityError
+                    raise CapacityError(f"rank {self.rank}: closure set full ({self.set_cap})")
                 self.S.add(key)
                 self.explored += 1
                 if key & self.bitj:

@@ -132,3 +132,43 @@ def test_partitioned_search_gloo_matches_oracle(world):
         assert p.exitcode == 0
     for r in range(world):
         assert [tuple(x) for x in got[r]] == exp, (r, got[r], exp)
+
+
+def _overflow_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lincheck import partition
+        from part_mock import MockPartPlan
+        out = []
+        for h in _part_histories()[:2]:
+            # only rank 1's sets are small: it overflows while rank 0 is mid-protocol
+            plan = MockPartPlan(h, rank=rank, world=world, set_cap=3 if rank == 1 else None)
+            r = partition.search(plan, tdist, "cpu", None)
+            out.append((r["valid"], r["err"]))
+        # the group is still usable afterwards (no collective was left unmatched)
+        t = __import__("torch").ones(1)
+        tdist.all_reduce(t)
+        out.append(float(t.item()))
+        q.put((rank, out))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_partitioned_overflow_on_one_rank_is_collective():
+    """a rank whose closure set overflows must not leave the others waiting in a
+    collective: every rank reports :unknown (LC_H_CAPACITY) at the same level."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overflow_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert got[r][:2] == [(2, -7), (2, -7)], (r, got[r])
+        assert got[r][2] == float(world)

@@ -196,3 +196,54 @@ def test_edn_round_trip_independent_history(tmp_path):
     assert back.keys == want.keys
     for a, b in zip(back.arrays(), want.arrays()):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("n_shards", [1, 2, 3, 8])
+def test_shard_histories_lpt(n_shards):
+    """lc_shard_histories (the split lc_check(n_gpus > 1) and bench --gpus N use) runs without
+    a device: every history lands on exactly one shard, deterministically, and the LPT bound
+    holds: no shard exceeds the mean load by more than the largest history."""
+    rng = np.random.default_rng(5)
+    sizes = rng.integers(0, 400, 97)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    h = H.History(off, *(np.zeros(int(off[-1]), t) for t in
+                         (np.int64, np.int32, np.int8, np.int8, np.int64, np.int64, np.int8)))
+    a = _lib.shard_histories(h, n_shards)
+    b = _lib.shard_histories(h, n_shards)
+    assert np.array_equal(a, b)
+    assert a.min() >= 0 and a.max() < n_shards
+    load = np.bincount(a, weights=sizes, minlength=n_shards)
+    assert load.max() <= sizes.sum() / n_shards + sizes.max()
+    if n_shards == 1:
+        assert np.all(a == 0)
+
+
+def test_shard_histories_rejects_bad_args():
+    L = _lib.load()
+    off = np.array([0, 5, 3], np.int64)  # not monotone
+    out = np.zeros(2, np.int32)
+    assert L.lc_shard_histories(2, _lib._p(off), 2, _lib._p(out)) == -1
+    assert L.lc_shard_histories(2, _lib._p(np.array([0, 1, 2], np.int64)), 0, _lib._p(out)) == -1
+
+
+def test_leader_model_routes_to_fallback():
+    """the :election workload's LeaderModel (leader.clj:63-85) is not
+    searched on the GPU; linearizable() hands back the documented fallback map."""
+    c = checker.linearizable({"model": model.LeaderModel(), "algorithm": "linear"})
+    r = c.check({}, [{"process": 0, "type": "invoke", "f": "inspect", "value": None, "index": 0}])
+    assert r["valid?"] == "unknown" and r["fallback"] == "knossos" and "error" in r
+    with pytest.raises(ValueError):
+        model.LeaderModel({1: "n1"})
+
+
+def test_independent_failures_exclude_unknown():
+    """jepsen.independent/checker lists keys whose :valid? is falsey; :unknown is truthy."""
+    class Fixed(checker.Checker):
+        def check(self, test, history, opts=None):
+            return {"valid?": {0: True, 1: "unknown", 2: False}[history[0]["value"]]}
+    ops = []
+    for k in range(3):
+        ops += [{"process": k, "type": "invoke", "f": "read", "value": H.KV(k, k), "index": 2 * k},
+                {"process": k, "type": "ok", "f": "read", "value": H.KV(k, k), "index": 2 * k + 1}]
+    r = checker.independent_checker(Fixed()).check({}, ops)
+    assert r["failures"] == [2] and r["valid?"] is False
