@@ -503,6 +503,7 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
 // the next step finds X | R at the word's own index. The OR of the X a step reads is step
 // t-1's post-return frontier: zero means step t-1 is the failing RETURN. An empty frontier
 // stays empty, so the steps started after a failure add no explored configs.
+constexpr int PIPE_SERIAL_SEGS = DENSE_PIPE_SERIAL_SEGS;
 constexpr int PIPE_OPN = 24;  // op-table entries per step: OP_PAD + slots 0..16, + the pull batches' tail
 struct __attribute__((aligned(16))) PipeStep {
   OpSel ops[PIPE_OPN];  // slot k at ops[OP_PAD + k]; every entry initialised
@@ -574,7 +575,9 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
   static_assert(OP_PAD + ((TLOG - 4) / 4) * 4 + 6 < PIPE_OPN && OP_PAD + TLOG <= PIPE_OPN, "op table too small");
   static_assert(RING <= 64, "one lane per ring entry");
   const int lane = threadIdx.x & 63;
-  const bool decoder = tt < 64;  // the team's first wave decodes the step headers
+  // the team's last wave decodes the step headers: packed passes fill the low threads first,
+  // so it has the fewest words of a super-layer
+  const bool decoder = tt >= TEAM - 64;
   for (;;) {
     if (tt == 0) *sQ = atomicAdd(p.queue, 1);
     team_sync<TEAM>();
@@ -594,12 +597,23 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
     int64_t pos = p.sbeg[h];
     if (ns > 0 && decoder) {
       pipe_decode(p, sw, pos, lane, &ring[0], nullptr);
-      if (tt == 0) ring[0].start = 0;
+      if (lane == 0) ring[0].start = 0;  // (the decoder wave, after its own stores)
     }
     team_sync<TEAM>();
     unsigned long long expl = 0;
     int fail_t = -1;
     int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0;  // decoded, started, retired
+    // LC_DEBUG: super-layer phase cycles of wave 0 and of the decoder wave (ring view + retire,
+    // segments, decode + start, barrier), s_memtime
+    const bool prof = p.lhist != nullptr && (tt == 0 || tt == TEAM - 64);
+    unsigned long long ph[4] = {0, 0, 0, 0}, tp = prof ? __builtin_amdgcn_s_memtime() : 0, nsl = 0;
+    auto mark = [&](int k) {
+      if (prof) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        ph[k] += t - tp;
+        tp = t;
+      }
+    };
     for (int s = 0; t_ret < ns; ++s) {
       // ---- ring view: lane i = step t_ret + i (decoded steps only)
       const int tl = t_ret + lane;
@@ -631,43 +645,40 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       uint32_t nq_l = 0, o_l = 0;
       if (seg_l) nq_l = binom[h1.z * BINOM_N + q_l], o_l = wofs[q_l];
       uint64_t segm = __ballot(seg_l);
-      if constexpr (TEAM == 64) {
-        // one wave: the segments' words are packed over the lanes (flat index f -> segment i,
-        // rank r), every lane with its own step's parameters, so a super-layer of several
-        // small layers is one pass instead of one pass per segment
-        uint32_t inc = nq_l;  // inclusive prefix of the word counts over the ring lanes
-#pragma unroll
-        for (int d = 1; d < RING; d <<= 1) {
-          const uint32_t v = (uint32_t)__shfl_up((int)inc, d, 64);
-          if (lane >= d) inc += v;
-        }
-        const uint32_t exc = inc - nq_l, total = rdl(inc, RING - 1);
-        // passes are wave-uniform: a shuffle reads 0 from an inactive source lane
-        for (uint32_t f0 = 0; f0 < total; f0 += 64u) {
-          const uint32_t f = f0 + (uint32_t)lane;
+      mark(0);
+      ++nsl;
+      if (!(p.pipe & PIPE_SERIAL_SEGS)) {
+        // packed: the running segments' words form one flat index f over the whole team
+        // (segment i = the ring lanes in order, its words at [e_i, e_i + nq_i)), so a
+        // super-layer of several small layers is ONE pass of every thread instead of one
+        // pass per segment; each thread reads its step's parameters from the ring in LDS
+        uint32_t total = 0;
+        for (uint64_t m = segm; m; m &= m - 1) total += rdl(nq_l, (int)__builtin_ctzll(m));
+        for (uint32_t f0 = 0; f0 < total; f0 += (uint32_t)TEAM) {
+          const uint32_t f = f0 + (uint32_t)tt;
           int i = 0;
+          uint32_t e = 0, acc = 0, o = 0;
           for (uint64_t m = segm; m; m &= m - 1) {
             const int k = (int)__builtin_ctzll(m);
-            if (f >= rdl(exc, k)) i = k;
+            if (f >= acc) i = k, e = acc, o = rdl(o_l, k);
+            acc += rdl(nq_l, k);
           }
-          const uint32_t r = f - (uint32_t)__shfl((int)exc, i, 64);
-          const uint32_t o = (uint32_t)__shfl((int)o_l, i, 64);
-          const uint32_t live = (uint32_t)__shfl((int)h0.x, i, 64), fresh = (uint32_t)__shfl((int)h0.y, i, 64);
-          const uint32_t foldm = (uint32_t)__shfl((int)h0.z, i, 64);
-          const int j = __shfl(h1.x, i, 64), jp = __shfl(h1.y, i, 64), H = __shfl(h1.z, i, 64);
-          const int t = t_ret_old + i;
           if (f >= total) continue;
-          const uint32_t w = words[o + r];
+          const uint32_t w = words[o + (f - e)];  // issued before the ring reads
+          const int t = t_ret_old + i;
+          PipeStep* st = &ring[t % RING];
+          const uint4 a = *reinterpret_cast<const uint4*>(&st->live);  // live, fresh, foldm, anyx
+          const int4 c = *reinterpret_cast<const int4*>(&st->j);       // j, jp, H, start
+          const uint32_t live = a.x, fresh = a.y, foldm = a.z;
           if (w & ~(live >> 3)) continue;
           uint64_t keep_lo = ~0ull;
 #pragma unroll
           for (int k = 0; k < 3; ++k)
             if (fresh & (1u << k)) keep_lo &= keep64(k);
-          PipeStep* st = &ring[t % RING];
           const OpSel* ops = st->ops + OP_PAD;
-          const uint64_t X = pipe_x(B, w, fresh >> 3, jp, keep_lo);
-          uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
-          R = close_in_word(X, w, live, j, ops, foldm, R);
+          const uint64_t X = pipe_x(B, w, fresh >> 3, c.y, keep_lo);
+          uint64_t R = pull_hi<4>(B, zero, w, c.x, c.z, ops, foldm);
+          R = close_in_word(X, w, live, c.x, ops, foldm, R);
           B[w] = X | R;
           expl += (uint32_t)__popcll(R);
           if (t > 0) st_fout += (uint32_t)__popcll(X);
@@ -678,7 +689,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       int i = segm ? (int)__builtin_ctzll(segm) : -1;
       uint32_t wn = 0;
       if (i >= 0 && (uint32_t)tt < rdl(nq_l, i)) wn = words[rdl(o_l, i) + tt];
-      while (i >= 0) {
+      while (i >= 0) {  // serial segments (PIPE_SERIAL_SEGS): one pass per segment
         segm &= segm - 1;
         const int i2 = segm ? (int)__builtin_ctzll(segm) : -1;
         uint32_t wn2 = 0;  // the next segment's first word, loaded ahead
@@ -710,6 +721,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
         if (nzx) st->anyx = 1;
         i = i2, wn = wn2;
       }
+      mark(1);
       // ---- decode ahead into a slot nobody read in this super-layer
       const int t_dec_old = t_dec;
       if (t_dec < ns && t_dec - t_ret_old < RING) {
@@ -726,7 +738,14 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
           ++t_run;
         }
       }
+      mark(2);
       team_sync<TEAM>();
+      mark(3);
+    }
+    if (prof) {
+      unsigned long long* q = p.lhist + 64 * LH_N + (TEAM == 64 ? 0 : TEAM >= 1024 ? 10 : 20) + (tt == 0 ? 0 : 5);
+      for (int k = 0; k < 4; ++k) atomicAdd(&q[k], ph[k]);
+      atomicAdd(&q[4], nsl);
     }
     if (fail_t < 0 && ns > 0) {  // the last step's return
       const PipeStep* st = &ring[(ns - 1) % RING];
@@ -974,8 +993,10 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
       if (decoder) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         long spins = 0;
-        while (!__all(lane >= G || poll_until(p, &flags[lane < G ? lane : 0], (unsigned long long)(s - 8), t0, spins)))
-          ;
+        for (int r0 = 0; r0 < G; r0 += 64)  // one lane per tile, 64 tiles at a time
+          while (!__all(r0 + lane >= G ||
+                        poll_until(p, &flags[r0 + lane < G ? r0 + lane : 0], (unsigned long long)(s - 8), t0, spins)))
+            ;
         if (tid == 0) *sAbort = ld_agent(p.abort);
       }
       __syncthreads();
@@ -1035,9 +1056,85 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     }
     uint64_t segm = __ballot(seg_l);
     const bool wide_any = __ballot(seg_l && lteam_l != 0) != 0;
-    // TW words per thread at a time, each chunk's word indices loaded one chunk ahead (the
-    // next segment's first chunk while this segment runs)
-    constexpr int TW = 2, TB = DENSE_WIDE_LMAX - DENSE_LMAX;
+    constexpr int TW = 2, TB = DENSE_TEAM_MAXB_SERIAL;
+    if (!(p.pipe & PIPE_SERIAL_SEGS)) {
+      constexpr int TB = DENSE_TEAM_MAXB;
+      // packed (as in history_pipe): one flat index over every running segment's words; each
+      // thread derives its step's parameters from the ring entry and this tile's rank
+      uint32_t total = 0;
+      for (uint64_t m = segm; m; m &= m - 1) total += rdl(nq_l, (int)__builtin_ctzll(m));
+      for (uint32_t f0 = 0; f0 < total; f0 += 1024u) {
+        const uint32_t f = f0 + (uint32_t)tid;
+        int i = 0;
+        uint32_t e = 0, acc = 0, o = 0;
+        for (uint64_t m = segm; m; m &= m - 1) {
+          const int k = (int)__builtin_ctzll(m);
+          if (f >= acc) i = k, e = acc, o = rdl(o_l, k);
+          acc += rdl(nq_l, k);
+        }
+        if (f >= total) continue;
+        const uint32_t w = p.words[o + (f - e)];  // issued before the ring reads
+        const int t = t_ret_old + i;
+        PipeStep* st = &ring[t % RING];
+        const uint4 a = *reinterpret_cast<const uint4*>(&st->live);  // live, fresh, foldm, anyx
+        const int4 c = *reinterpret_cast<const int4*>(&st->j);       // j, jp, H, start
+        const int2 d = *reinterpret_cast<const int2*>(&st->pstart);  // pstart, hp
+        const uint32_t live = a.x, fresh = a.y, foldm = a.z;
+        const int j = c.x, jp = c.y, H = c.z, q = s - c.w;
+        const uint32_t r = f - e;
+        const uint32_t live_loc = live & lmask, lteam = live >> lb;
+        if (w & ~(live_loc >> 3)) continue;
+        const bool wide = lteam != 0;
+        const int jt = j >= lb ? j - lb : -1;
+        const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
+        const bool jloc_hi = j >= 3 && j < lb;
+        const bool tile_fresh = ((uint32_t)rank & (fresh >> lb)) != 0;  // the tile's masks start empty
+        const uint32_t pmask = !wide ? 0u : tile_j ? (1u << jt) : ((uint32_t)rank & lteam);
+        const int xs = (jp >= lb && !tile_fresh) ? (rank | (1 << (jp - lb))) : -1;
+        uint64_t keep_lo = ~0ull;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          if (fresh & (1u << k)) keep_lo &= keep64(k);
+        const uint32_t fresh_hi = (fresh & lmask) >> 3;
+        const OpSel* ops = st->ops + OP_PAD;
+        if (!wide && xs < 0) {  // a step on this tile alone (then tile 0, jp local): LDS only
+          const uint64_t X = pipe_x(B, w, fresh_hi, jp, keep_lo);
+          uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+          R = close_in_word(X, w, live_loc, j, ops, foldm, R);
+          B[w] = X | R;
+          expl += (uint32_t)__popcll(R);
+          if (t > 0) st_fout += (uint32_t)__popcll(X);
+          if (X) st->anyx = 1;
+          continue;
+        }
+        const bool fx = !tile_fresh && !(w & fresh_hi);
+        // HBM loads first (X from tile xs, one pull per predecessor tile), used after
+        uint64_t xv = 0, pv[TB];
+        if (fx && xs >= 0) xv = HbmTab::ld(mirror(xs, t - 1) + cum[d.y * BINOM_N + min(q, d.y)] + r);
+        const uint32_t mo = cum[H * BINOM_N + q];
+        // pulls from the tiles one team bit below: none for masks holding a local j (never
+        // expanded); a tile holding j takes only T_j of r \ j
+        const bool pl = tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u));
+#pragma unroll
+        for (int b = 0; b < TB; ++b)
+          pv[b] = (pl && ((pmask >> b) & 1u)) ? HbmTab::ld(mirror(rank ^ (1 << b), t) + mo + r) : 0ull;
+        uint64_t X = xs >= 0 ? (xv & keep_lo) : (fx && jp < lb) ? pipe_x(B, w, 0u, jp, keep_lo) : 0ull;
+        uint64_t R = tile_j ? 0ull : pull_hi<4>(B, zero, w, j, H, ops, foldm);
+#pragma unroll
+        for (int b = 0; b < TB; ++b)
+          if ((pmask >> b) & 1u) R |= transfer(ops[lb + b], (foldm >> (lb + b)) & 1u, pv[b]);
+        if (!tile_j) R = close_in_word(X, w, live_loc, j, ops, foldm, R);
+        const uint64_t nv = X | R;
+        B[w] = nv;
+        if (wide) HbmTab::st(mirror(rank, t) + mo + r, nv);
+        expl += (uint32_t)__popcll(R);
+        if (t > 0) st_fout += (uint32_t)__popcll(X);
+        if (X) st->anyx = 1;
+      }
+      segm = 0;
+    }
+    // serial segments (PIPE_SERIAL_SEGS): TW words per thread at a time, each chunk's word
+    // indices loaded one chunk ahead (the next segment's first chunk while this segment runs)
     int i = segm ? (int)__builtin_ctzll(segm) : -1;
     uint32_t wn[TW];
 #pragma unroll
@@ -1190,6 +1287,46 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   }
 }
 
+// WAVE histories inside a big workgroup (DenseParams.n_w > 0, host knob LC_WAVE_IN_BIG): each
+// of its 16 waves is a WAVE team (history_pipe<64>, as in dense_wave_kernel) on its own 2 KiB
+// slice of the workgroup's LDS table, dequeuing from the WAVE queue. Running them here instead
+// of in dense_wave_kernel keeps that kernel's workgroups off the CUs: beside a big workgroup
+// of the pipelined-team instantiation (121 VGPRs, 4 waves per SIMD) no other wave fits, so
+// every CU a wave workgroup held was closed to the big kernel until the wave pool ended.
+__device__ __forceinline__ void big_wave_mode(const DenseParams& p, uint64_t* sTab, const uint64_t* zero,
+                                              const uint32_t* binom, int tid, unsigned long long& st_fout,
+                                              unsigned long long& st_steps) {
+  constexpr int NWV = 16, HW = DENSE_WAVE_LMAX - 3, TABW = 1 << HW;
+  uint64_t* const tabs = sTab;                                         // NWV tables of TABW words
+  PipeStep* const rings = reinterpret_cast<PipeStep*>(sTab + NWV * TABW);  // NWV rings
+  uint32_t* const words = reinterpret_cast<uint32_t*>(rings + NWV * WAVE_RING);  // HW-bit word list
+  uint32_t* const wofs = words + TABW;                                 // its layer offsets
+  int* const sQw = reinterpret_cast<int*>(wofs + 16);
+  unsigned long long* const sEx = reinterpret_cast<unsigned long long*>(sQw + NWV);
+  static_assert((NWV * TABW) * 8 + NWV * WAVE_RING * sizeof(PipeStep) + TABW * 4 + 16 * 4 + NWV * 4 + NWV * 8 <=
+                (1 << (DENSE_LMAX - 3)) * 8, "wave mode fits the big table");
+  __syncthreads();  // the table's previous users are done
+  if (tid <= HW + 1) {
+    uint32_t o = 0;
+    for (int q = 0; q < tid; ++q) o += binom[HW * BINOM_N + q];
+    wofs[tid] = o;
+  }
+  __syncthreads();
+  for (int v = tid; v < TABW; v += 1024) {  // colex rank within its popcount layer
+    uint32_t rank = 0;
+    int i = 0;
+    for (uint32_t x = (uint32_t)v; x; x &= x - 1, ++i) rank += binom[__builtin_ctz(x) * BINOM_N + i + 1];
+    words[wofs[__popc(v)] + rank] = (uint32_t)v;
+  }
+  __syncthreads();
+  DenseParams q = p;
+  q.n = p.n_w, q.order = p.order_w, q.queue = p.queue_w;
+  const int w = tid / 64;
+  history_pipe<64, DENSE_WAVE_LMAX, WAVE_RING>(q, tabs + w * TABW, zero, rings + w * WAVE_RING, &sQw[w], &sEx[w],
+                                               words, wofs, binom, tid & 63, st_fout, st_steps);
+  __syncthreads();
+}
+
 // BLOCK histories and TILE teams in one launch (same 1024-thread, 128 KiB-LDS workgroups, so
 // every workgroup is resident: the grid never exceeds one workgroup per CU).
 //
@@ -1232,6 +1369,10 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   unsigned long long st_fout = 0, st_steps = 0;
 
   if ((int)blockIdx.x >= p.n_team_wgs) {  // ------------------------------- BLOCK histories
+    // the last ceil(n_w / 16) workgroups start on the WAVE queue: a WAVE history is a long
+    // latency-bound chain, and started after the BLOCK queue it would be the launch's tail
+    if (p.n_w > 0 && (int)blockIdx.x >= (int)gridDim.x - (p.n_w + 15) / 16)
+      big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     if (p.pipe & 1) {
       history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
                                                  st_fout, st_steps);
@@ -1242,6 +1383,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     } else
       history_loop<1024, DENSE_LMAX>(p, sTab, &sZero, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout,
                                      st_steps);
+    if (p.n_w > 0) big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);  // then the WAVE queue
     flush_stats(p, st_fout, st_steps, tid == 0);
     return;
   }
@@ -1285,6 +1427,12 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     }
     const unsigned long long e = block_sum(expl, &sRed);
     if (tid == 0 && e) atomicAdd(&p.explored[h], e);
+    // the team is done (every tile passed its final barrier; other tiles read only this tile's
+    // HBM mirror): join the BLOCK queue, then the WAVE queue
+    __syncthreads();
+    history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
+                                               st_fout, st_steps);
+    if (p.n_w > 0) big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     flush_stats(p, st_fout, st_steps, tid == 0);
     return;
   }
@@ -1586,6 +1734,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     q2.n = p.n2, q2.order = p.order2, q2.queue = p.queue2;
     history_pipe<1024, DENSE_LMAX, BLOCK_RING>(q2, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
                                                st_fout, st_steps);
+    if (p.n_w > 0) big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
   }
   flush_stats(p, st_fout, st_steps, tid == 0);
 }

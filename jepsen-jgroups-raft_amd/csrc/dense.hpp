@@ -21,6 +21,9 @@ constexpr int DENSE_WIDE_LMAX = 22;  // widest table a tile team holds (2^(22-17
 constexpr int DENSE_MAX_STATES = 8;  // register values (state ids) per history
 constexpr int DENSE_WORD_BITS = DENSE_WIDE_LMAX - 3;  // bits of the sorted word list
 constexpr int DENSE_MRING = 32;      // mirror slots per tile (pipelined tile teams)
+constexpr int DENSE_TEAM_MAXB = 7;   // team bits of a pipelined tile team (packed segments)
+constexpr int DENSE_TEAM_MAXB_SERIAL = DENSE_WIDE_LMAX - DENSE_LMAX;  // ... with serial segments
+constexpr int DENSE_PIPE_SERIAL_SEGS = 32;  // DenseParams.pipe bit 5: one pass per segment
 
 // Step stream (host-built, one u32 word stream per history):
 //   header  live[0:22) | j[22:27) | ninv[27:32)   live = pending slots after this step's
@@ -65,6 +68,9 @@ struct DenseParams {
   uint32_t* team_any;           // pipelined teams: per team, bit t = some tile read a nonzero
   const int32_t* team_any_off;  // frontier in step t (step ns: the last return); word offsets
   unsigned long long* done;      // [n_team_wgs] team steps finished (LC_PIPE bit 3)
+  int32_t n_w;                  // big kernel: WAVE histories its waves run after the BLOCK
+  const int32_t* order_w;       // queue (0: dense_wave_kernel runs them)
+  int32_t* queue_w;
   int32_t pipe;                 // bit 3: tile teams without per-step team barriers;
                                 // bit 0: BLOCK, bit 1: WAVE, bit 2: TILE teams overlap
                                 // consecutive steps (history_pipe / team_pipe); default 11

@@ -140,8 +140,12 @@ struct lc_plan {
   int wide_from = 99, wide_lbits = DENSE_LMAX;        // LC_TILE_WIDE=w:b: b local slots from width w
   // LC_PIPE: bits 0/1/2 = BLOCK/WAVE/TILE teams overlap steps (0: one at a time); bit 3 = tile
   // teams without per-step team barriers (finished teams then join the BLOCK queue); bit 4 =
-  // MID teams for widths 12..14 (needs bit 0)
-  int dense_pipe = 11;
+  // MID teams for widths 12..14 (needs bit 0); bit 5 = one pass per running segment (r1 form;
+  // default: segments packed over the team); bit 6 = WAVE histories on the big kernel's waves
+  // (no dense_wave_kernel). Default 79 = 1|2|4|8|64, with the team planner (plan_teams).
+  int dense_pipe = 79;
+  std::vector<int> plan_lb;  // team planner: local slots per tile (0: not a team)
+  bool plan_off = false;     // LC_TEAM_PLAN=0: every wide history keeps 17-bit tiles
   hipStream_t stream2 = nullptr, stream3 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_b0 = nullptr, ev_b1 = nullptr, ev_w0 = nullptr, ev_w1 = nullptr;  // per dense kernel
@@ -250,6 +254,8 @@ struct lc_plan {
     if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e);
+    if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
+    if ((e = getenv("LC_PLAN_K")) && atof(e) > 0) plan_k16 = atof(e);
     if ((e = getenv("LC_TILE_WIDE")) && strchr(e, ':')) {
       wide_from = atoi(e);
       wide_lbits = std::max(12, std::min(atoi(strchr(e, ':') + 1), DENSE_LMAX));
@@ -341,8 +347,10 @@ struct lc_plan {
     std::vector<int32_t> nst(n, 0);
     std::vector<int8_t> lm(n, 0);
     std::vector<double> cost(n, 0.0);
+    std::vector<std::vector<uint8_t>> widths(n);  // per step live width (team planner)
     dalg_off.assign(n + 1, 0);
     dalg.clear();
+    plan_lb.assign(n, 0);
     for (int h = 0; h < n; ++h) {
       dalg_off[h] = (int64_t)dalg.size();
       if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || enc.live_max[h] > dense_maxw) continue;
@@ -365,6 +373,7 @@ struct lc_plan {
         }
         const int L = 32 - __builtin_clz(live);
         cost[h] += (double)(1u << L) * L;
+        widths[h].push_back((uint8_t)L);
         dalg.push_back(step_alg_bytes(live, (int)(q1 - q0)));
       }
       const int lw = enc.live_max[h];
@@ -372,6 +381,7 @@ struct lc_plan {
       (lw <= DENSE_WAVE_LMAX ? dense_w : (lw <= DENSE_MID_LMAX && (dense_pipe & 17) == 17) ? dense_m
        : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
     }
+    plan_teams(widths);
     auto heavy_first = [&](int a, int b) { return cost[a] > cost[b]; };
     std::stable_sort(dense_b.begin(), dense_b.end(), heavy_first);
     std::stable_sort(dense_w.begin(), dense_w.end(), heavy_first);
@@ -399,6 +409,88 @@ struct lc_plan {
     HIP_TRY(d_dfail.ensure((size_t)std::max(n, 1) * 4));
     HIP_TRY(d_dexpl.ensure((size_t)std::max(n, 1) * 8));
     return 0;
+  }
+
+  // Team planner (pipelined tile teams, LC_PIPE bits 2|3): how many local slots each tile of a
+  // team holds. A history's time is the chain of its steps, so the launch lasts as long as the
+  // slowest history, or the pool (BLOCK histories, heaviest first, then WAVE histories 16 per
+  // workgroup) on the workgroups the teams leave, whichever is later. Greedy: while the slowest
+  // single history bounds that makespan, give it tiles of one slot fewer (twice the
+  // workgroups; a BLOCK history becomes a 2-tile team) if that shortens it and the pool, on
+  // fewer workgroups, still ends before the new makespan. Step-time models (us; least-squares
+  // fits to MI355X LC_DEBUG history times, r2c-r2h), L = the step's live width:
+  //   BLOCK step   4.67 + 0.00266 * 2^(L-3)
+  //   team step    1.59 + 0.0043 * 2^(min(L,lb)-3) + (L > lb) * (3.87 + 1.57 * (L - lb))
+  //   WAVE step    7.9 (16 histories share a workgroup)
+  static double est_block_us(const std::vector<uint8_t>& ws) {
+    double t = 0;
+    for (uint8_t L : ws) t += 4.67 + 0.00266 * std::ldexp(1.0, std::max(0, (int)L - 3));
+    return t;
+  }
+  double plan_k16 = 1.0;  // LC_PLAN_K: scales the team model's VALU term (calibration runs)
+  double est_team_us(const std::vector<uint8_t>& ws, int lb) const {
+    double t = 0;
+    for (uint8_t L : ws) {
+      t += 1.59 + 0.0043 * plan_k16 * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
+      if (L > lb) t += 3.87 + 1.57 * (L - lb);
+    }
+    return t;
+  }
+  void plan_teams(const std::vector<std::vector<uint8_t>>& ws) {
+    const bool pipe_teams = (dense_pipe & 12) == 12;
+    const int maxb = (dense_pipe & DENSE_PIPE_SERIAL_SEGS) ? DENSE_TEAM_MAXB_SERIAL : DENSE_TEAM_MAXB;
+    const int cap = std::min(dgrid_b, tile_cap);
+    for (int h : dense_x) plan_lb[h] = DENSE_LMAX;
+    if (!pipe_teams || getenv("LC_TILE_LBITS") || getenv("LC_TILE_WIDE") || plan_off) return;
+    auto wgs = [&](int h, int lb) { return enc.live_max[h] > lb ? 1 << (enc.live_max[h] - lb) : 1; };
+    std::vector<double> est(enc.n_hist, 0.0);
+    std::vector<char> in_block(enc.n_hist, 0);
+    int team_wgs = 0;
+    for (int h : dense_x) team_wgs += wgs(h, DENSE_LMAX), est[h] = est_team_us(ws[h], DENSE_LMAX);
+    double pool = 0;
+    for (int h : dense_b) in_block[h] = 1, est[h] = est_block_us(ws[h]), pool += est[h];
+    if (dense_pipe & 64)  // WAVE histories on the big kernel's waves, 16 per workgroup
+      for (int h : dense_w) pool += 7.9 * (double)ws[h].size() / 16.0;
+    std::vector<int> cand(dense_x);
+    for (int h : dense_b)
+      if (enc.live_max[h] >= 14) cand.push_back(h);
+    for (int iter = 0; iter < 4096 && !cand.empty(); ++iter) {
+      int best = cand[0];
+      for (int h : cand) if (est[h] > est[best]) best = h;
+      const int block_wgs = std::max(1, dgrid_b - team_wgs);
+      if (est[best] <= pool / block_wgs) break;  // the pool bounds the launch
+      const int lw = enc.live_max[best];
+      const int cur = in_block[best] ? lw : plan_lb[best];
+      double second = 0;  // the slowest other history
+      for (int h : cand) if (h != best) second = std::max(second, est[h]);
+      // every smaller tile size the team limits allow: the one with the smallest makespan
+      int nlb = -1, extra = 0;
+      double t_new = est[best], m_best = est[best];
+      for (int lb = cur - 1; lb >= 13 && lw - lb <= maxb; --lb) {
+        const int x = wgs(best, lb) - (in_block[best] ? 1 : wgs(best, cur));
+        if (team_wgs + x > cap || dgrid_b - team_wgs - x < 1) break;
+        const double t = est_team_us(ws[best], lb);
+        const double pool_new = (pool - (in_block[best] ? est[best] : 0.0)) / (dgrid_b - team_wgs - x);
+        const double m = std::max(std::max(t, second), pool_new);
+        if (m < m_best - 1.0) nlb = lb, extra = x, t_new = t, m_best = m;
+      }
+      if (nlb < 0) break;
+      if (in_block[best]) {
+        in_block[best] = 0;
+        pool -= est[best];
+        dense_b.erase(std::find(dense_b.begin(), dense_b.end(), best));
+        dense_x.push_back(best);
+      }
+      team_wgs += extra;
+      plan_lb[best] = nlb;
+      est[best] = t_new;
+    }
+    if (debug()) {
+      fprintf(stderr, "[lincheck] team plan: %zu teams, %d team workgroups, block pool est %.0f us on %d wgs:",
+              dense_x.size(), team_wgs, pool / std::max(1, dgrid_b - team_wgs), dgrid_b - team_wgs);
+      for (int h : dense_x) fprintf(stderr, " h%d:w%d/lb%d(%.0fus)", h, enc.live_max[h], plan_lb[h], est[h]);
+      fprintf(stderr, "\n");
+    }
   }
 
   // Dense closure-table kernels: the big kernel (tile teams first, then BLOCK histories) on
@@ -431,8 +523,8 @@ struct lc_plan {
       HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
       HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
       p.stamps = d_dstamps.as<unsigned long long>();
-      HIP_TRY(d_dlhist.ensure(64 * LH_N * 8));
-      HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, 64 * LH_N * 8, stream));
+      HIP_TRY(d_dlhist.ensure((64 * LH_N + 32) * 8));
+      HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, (64 * LH_N + 32) * 8, stream));
       p.lhist = d_dlhist.as<unsigned long long>();
     }
     // tile teams: one per wide history, 2^(width - 17) workgroups; packed into launches of at
@@ -446,6 +538,7 @@ struct lc_plan {
     while ((2 << grid_log) <= dgrid_b) ++grid_log;
     auto lbits_of = [&](int h) {
       const int lw = enc.live_max[h];
+      if (plan_lb[h] > 0 && plan_lb[h] < DENSE_LMAX) return plan_lb[h];  // team planner
       const int want = lw >= wide_from ? std::min(wide_lbits, tile_lbits) : tile_lbits;
       return std::min(DENSE_LMAX, std::max(lw - grid_log, std::min(want, lw - 1)));
     };
@@ -492,12 +585,12 @@ struct lc_plan {
       }
       max_anyw = std::max(max_anyw, (size_t)o);
     }
-    // pipelined teams pull over at most DENSE_WIDE_LMAX - DENSE_LMAX team bits per tile
+    // pipelined teams pull over at most DENSE_TEAM_MAXB team bits per tile (5 with serial segments)
     // (LC_TILE_LBITS below 17 can make more): such launches use the per-step team loop
     int pipe_mode = dense_pipe;
     for (size_t l = 0; l < launches.size(); ++l)
       for (int8_t t : l_bits[l])
-        if (t > DENSE_WIDE_LMAX - DENSE_LMAX) pipe_mode &= ~4;
+        if (t > ((dense_pipe & DENSE_PIPE_SERIAL_SEGS) ? DENSE_TEAM_MAXB_SERIAL : DENSE_TEAM_MAXB)) pipe_mode &= ~4;
     p.pipe = pipe_mode;
     if (max_wgs) {
       const size_t slots = (pipe_mode & 4) ? DENSE_MRING : 2;  // 2: the per-step loop's buffers
@@ -515,8 +608,10 @@ struct lc_plan {
       HIP_TRY(d_thist.ensure(max_teams * 4));
       HIP_TRY(hipMemsetAsync(d_abort.p, 0, 16, stream));
     }
+    // LC_PIPE bit 6 (default): WAVE histories run on the big kernel's waves after its BLOCK queue
+    const bool wave_in_big = (dense_pipe & 64) != 0;
     HIP_TRY(hipEventRecord(ev0, stream));
-    if (nw) {
+    if (nw && !wave_in_big) {
       HIP_TRY(hipEventRecord(ev_fork, stream));
       HIP_TRY(hipStreamWaitEvent(stream2, ev_fork, 0));
       DenseParams q = p;
@@ -530,7 +625,7 @@ struct lc_plan {
       HIP_TRY(hipEventRecord(ev_join, stream2));
     }
     if (nm) {
-      if (!nw) HIP_TRY(hipEventRecord(ev_fork, stream));
+      if (!nw || wave_in_big) HIP_TRY(hipEventRecord(ev_fork, stream));
       HIP_TRY(hipStreamWaitEvent(stream3, ev_fork, 0));
       DenseParams q = p;
       q.n = nm;
@@ -540,7 +635,7 @@ struct lc_plan {
       HIP_TRY(hipEventRecord(ev_m0, stream3));
       // wave + MID workgroups stay within one per CU: either fits beside a big-kernel
       // workgroup, two of them do not, and every tile-team workgroup must be resident
-      const int wgrid = nw ? std::min(dgrid_w, (nw + 3) / 4) : 0;
+      const int wgrid = nw && !wave_in_big ? std::min(dgrid_w, (nw + 3) / 4) : 0;
       const int mgrid = std::min(nm, dgrid_m - wgrid);
       if (mgrid > 0) HIP_TRY(launch_dense(q, DENSE_MID, mgrid, stream3));
       HIP_TRY(hipEventRecord(ev_m1, stream3));
@@ -557,6 +652,12 @@ struct lc_plan {
       q.order2 = d_dorder.as<int32_t>() + nb + nw + nx;
       q.queue2 = d_dqueue.as<int32_t>() + 2;
       q.n_team_wgs = twgs;
+      q.n_w = 0;
+      if (l == 0 && wave_in_big) {
+        q.n_w = nw;
+        q.order_w = d_dorder.as<int32_t>() + nb;
+        q.queue_w = d_dqueue.as<int32_t>() + 1;
+      }
       if (nt) {
         HIP_TRY(hipMemcpyAsync(d_wgteam.p, l_wgteam[l].data(), twgs * 4, hipMemcpyHostToDevice, stream));
         HIP_TRY(hipMemcpyAsync(d_tbase.p, l_base[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
@@ -586,11 +687,11 @@ struct lc_plan {
           q.tstamps = d_tstamps.as<unsigned long long>();
         }
       }
-      const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n + q.n2));
+      const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n + q.n2 + (q.n_w + 15) / 16));
       if (grid > 0) HIP_TRY(launch_dense(q, DENSE_BIG, grid, stream));
     }
     HIP_TRY(hipEventRecord(ev_b1, stream));
-    if (nw) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
+    if (nw && !wave_in_big) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
     if (nm) HIP_TRY(hipStreamWaitEvent(stream, ev_join3, 0));
     HIP_TRY(hipEventRecord(ev1, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -615,14 +716,14 @@ struct lc_plan {
     for (int i = 0; i < SS_N; ++i) ss[i] = ss3[i] + ss3[SS_N + i] + ss3[2 * SS_N + i];
     for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
       for (int h : *ids) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
-    stats[1] += (nw ? 1 : 0) + (nm ? 1 : 0) + (double)launches.size();
+    stats[1] += (nw && !wave_in_big ? 1 : 0) + (nm ? 1 : 0) + (double)launches.size();
     stats[12] += nb + nw + nx + nm;
     stats[13] += t;
     // per-kernel time (events on each kernel's own stream) and algorithmic bytes of the steps
     // each kernel ran: 14/15 big/wave ms, 16/17 big HBM/LDS bytes, 18/19 wave HBM/LDS bytes
     float tb = 0, tw = 0;
     HIP_TRY(hipEventElapsedTime(&tb, ev_b0, ev_b1));
-    if (nw) HIP_TRY(hipEventElapsedTime(&tw, ev_w0, ev_w1));
+    if (nw && !wave_in_big) HIP_TRY(hipEventElapsedTime(&tw, ev_w0, ev_w1));
     float tm = 0;  // the MID kernel runs beside both; its steps are counted with the wave kernel's
     if (nm) HIP_TRY(hipEventElapsedTime(&tm, ev_m0, ev_m1));
     stats[14] += tb;
@@ -630,7 +731,7 @@ struct lc_plan {
     for (const std::vector<int>* ids : {&dense_b, &dense_x, &dense_w, &dense_m})
       for (int h : *ids) {
         const StepBytes b = dense_hist_bytes(h, fs[h]);
-        const int k = (ids == &dense_w || ids == &dense_m) ? 18 : 16;
+        const int k = ((ids == &dense_w && !wave_in_big) || ids == &dense_m) ? 18 : 16;
         stats[k] += b.hbm;
         stats[k + 1] += b.lds;
       }
@@ -642,12 +743,13 @@ struct lc_plan {
     {
       double ex_big = 0, ex_wave = 0;
       for (const std::vector<int>* ids : {&dense_b, &dense_x}) for (int h : *ids) ex_big += (double)ex[h];
-      for (const std::vector<int>* ids : {&dense_w, &dense_m}) for (int h : *ids) ex_wave += (double)ex[h];
+      for (const std::vector<int>* ids : {&dense_w, &dense_m})
+        for (int h : *ids) (ids == &dense_w && wave_in_big ? ex_big : ex_wave) += (double)ex[h];
       const double fo_big = (double)ss3[SS_FOUT], fo_wave = (double)(ss3[SS_N + SS_FOUT] + ss3[2 * SS_N + SS_FOUT]);
-      stats[25] += fo_big + (nb + nx);
+      stats[25] += fo_big + (nb + nx + (wave_in_big ? nw : 0));
       stats[26] += fo_big;
       stats[27] += ex_big;
-      stats[28] += fo_wave + (nw + nm);
+      stats[28] += fo_wave + ((wave_in_big ? 0 : nw) + nm);
       stats[29] += fo_wave;
       stats[30] += ex_wave;
     }
@@ -656,7 +758,17 @@ struct lc_plan {
               "workgroups): %.3f ms, steps=%llu Fout=%llu\n", nb, nw, nx, launches.size(), max_wgs, t,
               ss[SS_STEPS], ss[SS_FOUT]);
       dense_report();
-      std::vector<unsigned long long> LH(64 * LH_N);
+      std::vector<unsigned long long> LH(64 * LH_N + 32);
+      if (hipMemcpy(LH.data(), d_dlhist.p, LH.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
+        for (int kind = 0; kind < 3; ++kind)
+          for (int wv = 0; wv < 2; ++wv) {
+            const unsigned long long* q = &LH[64 * LH_N + kind * 10 + wv * 5];
+            if (!q[4]) continue;
+            const double n = (double)q[4];
+            fprintf(stderr, "[lincheck]   pipelined %s teams, %s: per super-layer cycles: ring %.0f segments %.0f "
+                    "decode+start %.0f barrier %.0f (%.0f super-layers)\n", kind == 0 ? "WAVE" : kind == 1 ? "BLOCK" : "MID",
+                    wv == 0 ? "wave 0" : "decoder wave", q[0] / n, q[1] / n, q[2] / n, q[3] / n, n);
+          }
       if (hipMemcpy(LH.data(), d_dlhist.p, LH.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
         for (int k = 0; k < 64; ++k) {
           const unsigned long long* e = &LH[k * LH_N];
@@ -667,17 +779,21 @@ struct lc_plan {
                   "of %d  explored %8.1f\n", k >= 32 ? "block" : "wave ", L, e[0], e[1] / s / 100.0, e[2] / s,
                   e[3] / s, 1 << (L > 3 ? L - 3 : 0), e[4] / s);
         }
-      if (!launches[0].empty()) {  // phase split of the first tile team (the heaviest history)
-        const int g0 = 1 << l_bits[0][0];
-        std::vector<unsigned long long> TS((size_t)g0 * 8);
+      if (!launches[0].empty()) {  // phase split of every tile team of the first launch
+        std::vector<unsigned long long> TS(l_wgteam[0].size() * 8);
         if (hipMemcpy(TS.data(), d_tstamps.p, TS.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
-          for (int r = 0; r < g0; ++r) {
-            const double st = std::max(1.0, (double)TS[r * 8 + 5]);
-            fprintf(stderr, (p.pipe & 4) ? "[lincheck]     tile team h=%d rank %2d: per super-layer us: wait %.2f "
-                    "compute %.2f publish %.2f credit %.2f - %.2f (%.0f super-layers)\n" : "[lincheck]     tile team "
-                    "h=%d rank %2d: per team step us: wait %.1f compute %.1f publish %.1f return %.1f barrier %.1f (%.0f steps)\n", l_hist[0][0], r, TS[r * 8] / st / 100,
-                    TS[r * 8 + 1] / st / 100, TS[r * 8 + 2] / st / 100, TS[r * 8 + 3] / st / 100,
-                    TS[r * 8 + 4] / st / 100, st);
+          for (size_t tm = 0; tm < l_hist[0].size(); ++tm) {
+            const int g0 = 1 << l_bits[0][tm], b0 = l_base[0][tm];
+            for (int r = 0; r < g0; ++r) {
+              if (r > 1 && r != g0 - 1 && tm > 0) continue;  // ranks 0, 1, last of later teams
+              const unsigned long long* T = &TS[(size_t)(b0 + r) * 8];
+              const double st = std::max(1.0, (double)T[5]);
+              fprintf(stderr, (p.pipe & 4) ? "[lincheck]     tile team h=%d lb=%d rank %2d: per super-layer us: wait %.2f "
+                      "compute %.2f publish %.2f credit %.2f - %.2f (%.0f super-layers)\n" : "[lincheck]     tile team "
+                      "h=%d lb=%d rank %2d: per team step us: wait %.1f compute %.1f publish %.1f return %.1f barrier %.1f (%.0f steps)\n",
+                      l_hist[0][tm], (int)l_lbits[0][tm], r, T[0] / st / 100, T[1] / st / 100, T[2] / st / 100,
+                      T[3] / st / 100, T[4] / st / 100, st);
+            }
           }
       }
     }

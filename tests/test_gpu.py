@@ -400,7 +400,25 @@ def test_gpu_dense_tables_vs_oracle():
     p.close()
 
 
-@pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "27"])
+@pytest.mark.parametrize("plan", ["1", "0"])
+def test_gpu_dense_team_planner(plan, monkeypatch):
+    """The team planner (LC_PIPE bits 2|3, the default): with few histories per GPU (as each
+    rank holds when C3's keys are split over 8 GPUs) the longest ones get smaller tiles, and
+    BLOCK-width histories (15..17) become 2-tile teams. Bit-exact with the oracle and with the
+    planner off (LC_TEAM_PLAN=0: 17-bit tiles for width > 17 only)."""
+    monkeypatch.setenv("LC_TEAM_PLAN", plan)
+    h = H.concat([synth.gen_register_keys(14, 1000, 5, 0.01, config_id=3, key0=250)] +
+                 [synth.gen_register(150, 5, 0.12, 31000 + t, invalid=True) for t in (0, 2, 5, 6)])
+    widths = [_live_width(h, k) for k in range(h.n_hist)]
+    assert any(15 <= w <= 17 for w in widths) and max(widths) > 17
+    g = _lib.check(1, 0, h)
+    exp = oracle.check_many("cas-register", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"plan={plan} w={widths[k]}")
+    assert any(e["valid"] == 0 for e in exp)
+
+
+@pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "15", "27", "47"])
 def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     """LC_PIPE bit 0 / bit 1: BLOCK / WAVE teams overlap consecutive RETURN steps (step t+1's
     layer q beside step t's layer q + 2, returns read through the previous step's slot, fresh
