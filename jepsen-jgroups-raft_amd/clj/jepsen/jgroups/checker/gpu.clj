@@ -68,6 +68,46 @@
                 :linearized (vec (for [x (range (aget n-lin c))] (aget lin (+ (* 64 c) x))))
                 :pending    pend}))))))
 
+(defn- folded-ops
+  "invocation :index -> the op as the model steps it (an :ok completion's :value folded into
+  its invocation, as knossos.history/complete does)."
+  [ops]
+  (loop [ops ops, open {}, out {}]
+    (if-let [o (first ops)]
+      (let [p (:process o)]
+        (if (= :invoke (:type o))
+          (recur (rest ops) (assoc open p (:index o)) (assoc out (:index o) o))
+          (let [i (open p)]
+            (recur (rest ops) (dissoc open p)
+                   (if (and i (= :ok (:type o))) (assoc-in out [i :value] (:value o)) out)))))
+      out)))
+
+(defn- final-paths
+  ":final-paths: from each pre-failure config, pending ops linearized one after another (each
+  step consistent), ending with the failing op's inconsistent step; breadth-first, <= k."
+  [m configs fail-inv ops k]
+  (let [folded  (folded-ops ops)
+        fop     (folded fail-inv)
+        pending (sort (:pending (first configs)))]
+    (when fop
+      (loop [queue (for [c configs]
+                     [(assoc m :value (get-in c [:model :value])) (set (:linearized c))
+                      [{:op nil :model (:model c)}]])
+             paths []]
+        (if (or (empty? queue) (>= (count paths) k))
+          (vec (take k paths))
+          (let [done (for [[mm _ path] queue
+                           :let [r (model/step mm fop)]
+                           :when (model/inconsistent? r)]
+                       (conj path {:op fop :model r}))
+                nxt  (for [[mm lin path] queue
+                           i pending
+                           :when (and (not (lin i)) (not= i fail-inv) (folded i))
+                           :let [r (model/step mm (folded i))]
+                           :when (not (model/inconsistent? r))]
+                       [r (conj lin i) (conj path {:op (folded i) :model r})])]
+            (recur nxt (into paths done))))))))
+
 (defn check-histories
   "One lc_check call for many histories; returns a vector of Knossos-keyed maps."
   [model-kind init histories opts]
@@ -96,7 +136,11 @@
                                  ;; linearization returns the previous :ok op last
                                  :last-op     (at (aget prev i)))
                (and (zero? v) (:configs opts true))
-               (assoc :configs (failure-configs i 10))))))))
+               ((fn [r]
+                  (let [cfgs (failure-configs i 10)]
+                    (cond-> (assoc r :configs cfgs)
+                      (seq cfgs) (assoc :final-paths
+                                        (final-paths (:model opts) cfgs (aget finv i) ops 10))))))))))))
 
 (defn- model-kind
   "[model_kind init] for the models the GPU implements, else nil (-> Knossos)."

@@ -236,11 +236,21 @@ struct lc_plan {
     if (!ev_join3) HIP_TRY(hipEventCreateWithFlags(&ev_join3, hipEventDisableTiming));
     for (hipEvent_t* e : {&ev_b0, &ev_b1, &ev_w0, &ev_w1, &ev_m0, &ev_m1})
       if (!*e) HIP_TRY(hipEventCreate(e));
-    nwg = search_grid_size(model);
-    dgrid_b = dense_grid_size(DENSE_BIG);
-    dgrid_w = dense_grid_size(DENSE_WAVE);
-    dgrid_m = dense_grid_size(DENSE_MID);
-    knwg = keys_grid_size(model);
+    {
+      // occupancy queries (hipGetDeviceProperties ~ms each) once per device and model; the
+      // caller holds the device mutex
+      static struct { bool ok; int nwg, db, dw, dm, knwg; } cache[64][3];
+      auto& c = cache[device & 63][model & 3];
+      if (!c.ok) {
+        c.nwg = search_grid_size(model);
+        c.db = dense_grid_size(DENSE_BIG);
+        c.dw = dense_grid_size(DENSE_WAVE);
+        c.dm = dense_grid_size(DENSE_MID);
+        c.knwg = keys_grid_size(model);
+        c.ok = c.nwg > 0 && c.knwg > 0;
+      }
+      nwg = c.nwg, dgrid_b = c.db, dgrid_w = c.dw, dgrid_m = c.dm, knwg = c.knwg;
+    }
     if (nwg <= 0 || knwg <= 0) {
       last_error = "search kernels cannot be resident (occupancy 0)";
       return LC_E_DEVICE;
@@ -348,15 +358,27 @@ struct lc_plan {
     std::vector<int8_t> lm(n, 0);
     std::vector<double> cost(n, 0.0);
     std::vector<std::vector<uint8_t>> widths(n);  // per step live width (team planner)
-    dalg_off.assign(n + 1, 0);
-    dalg.clear();
     plan_lb.assign(n, 0);
+    // sizes first (one header per step plus one word per invocation), then every history's
+    // stream filled in parallel into its own range
+    std::vector<char> ok(n, 0);
+    dalg_off.assign(n + 1, 0);
+    std::vector<int64_t> wcount(n + 1, 0);
     for (int h = 0; h < n; ++h) {
-      dalg_off[h] = (int64_t)dalg.size();
-      if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || enc.live_max[h] > dense_maxw) continue;
-      sbeg[h] = (int64_t)words.size();
+      ok[h] = !enc.err[h] && enc.n_states[h] <= DENSE_MAX_STATES && enc.live_max[h] <= dense_maxw;
+      const int64_t s0 = enc.step_off[h], s1 = enc.step_off[h + 1];
+      dalg_off[h + 1] = dalg_off[h] + (ok[h] ? s1 - s0 : 0);
+      wcount[h + 1] = wcount[h] + (ok[h] ? (s1 - s0) + (enc.inv_off[s1] - enc.inv_off[s0]) : 0);
+    }
+    words.resize(wcount[n]);
+    dalg.assign(dalg_off[n], StepBytes{0, 0});
+    auto fill = [&](int h) {
+      if (!ok[h]) return;
+      sbeg[h] = wcount[h];
       nst[h] = enc.n_steps(h);
       lm[h] = (int8_t)std::max(1, enc.live_max[h]);
+      widths[h].resize(nst[h]);
+      uint32_t* out = words.data() + wcount[h];
       uint32_t live = 0;
       for (int t = 0; t < nst[h]; ++t) {
         const int64_t g = (int64_t)enc.step_off[h] + t;
@@ -364,18 +386,29 @@ struct lc_plan {
         const int64_t q0 = enc.inv_off[g], q1 = enc.inv_off[g + 1];
         for (int64_t q = q0; q < q1; ++q) live |= 1u << enc.inv_slot[q];
         const uint32_t j = enc.step_slot[g];
-        words.push_back(live | (j << 22) | ((uint32_t)(q1 - q0) << 27));
+        *out++ = live | (j << 22) | ((uint32_t)(q1 - q0) << 27);
         for (int64_t q = q0; q < q1; ++q) {
           const int64_t a = enc.inv_a[q], b = enc.inv_b[q];
           const uint32_t am = a == R_ANY ? 0xffu : (a == R_NEVER ? 0u : (1u << a));
           const uint32_t bm = b < 0 ? 0u : (1u << b);
-          words.push_back((uint32_t)enc.inv_slot[q] | (am << 8) | (bm << 16));
+          *out++ = (uint32_t)enc.inv_slot[q] | (am << 8) | (bm << 16);
         }
         const int L = 32 - __builtin_clz(live);
         cost[h] += (double)(1u << L) * L;
-        widths[h].push_back((uint8_t)L);
-        dalg.push_back(step_alg_bytes(live, (int)(q1 - q0)));
+        widths[h][t] = (uint8_t)L;
+        dalg[dalg_off[h] + t] = step_alg_bytes(live, (int)(q1 - q0));
       }
+    };
+    {
+      const int nt = wcount[n] > 200000 ? (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
+      std::vector<std::thread> th;
+      for (int w = 1; w < nt; ++w)
+        th.emplace_back([&, w] { for (int h = w; h < n; h += nt) fill(h); });
+      for (int h = 0; h < n; h += nt) fill(h);
+      for (auto& t : th) t.join();
+    }
+    for (int h = 0; h < n; ++h) {
+      if (!ok[h]) continue;
       const int lw = enc.live_max[h];
       // MID teams (several per CU) take the narrower BLOCK histories when BLOCK steps are pipelined
       (lw <= DENSE_WAVE_LMAX ? dense_w : (lw <= DENSE_MID_LMAX && (dense_pipe & 17) == 17) ? dense_m
@@ -391,7 +424,6 @@ struct lc_plan {
     ord.insert(ord.end(), dense_w.begin(), dense_w.end());
     ord.insert(ord.end(), dense_x.begin(), dense_x.end());
     ord.insert(ord.end(), dense_m.begin(), dense_m.end());
-    dalg_off[n] = (int64_t)dalg.size();
     dstream_words = (int64_t)words.size();
     int rc;
     if ((rc = upload(d_dstream, words))) return rc;
@@ -1227,16 +1259,22 @@ struct lc_plan {
 
 namespace {
 
+// Encode histories and upload them into plan `reuse` (its device buffers, streams and events
+// kept: lc_check's per-device cached plan) or into a new plan.
 int plan_build(int device, int model, int64_t init_value, int n_hist, const int64_t* hist_off,
-               const HistArrays& a, int64_t max_configs, lc_plan** out, std::string& msg) {
+               const HistArrays& a, int64_t max_configs, lc_plan** out, std::string& msg,
+               lc_plan* reuse = nullptr) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) {
     return std::chrono::duration<double, std::milli>(clk::now() - t).count();
   };
-  auto p = std::make_unique<lc_plan>();
+  std::unique_ptr<lc_plan> fresh(reuse ? nullptr : new lc_plan());
+  lc_plan* const p = reuse ? reuse : fresh.get();
   p->device = device;
   p->model = model;
   p->max_configs = max_configs;
+  p->max_t = INT32_MAX;
+  std::fill(p->phase_ms, p->phase_ms + 5, 0.0);
   auto t = clk::now();
   encode(model, init_value, n_hist, hist_off, a, p->enc);
   p->phase_ms[0] = ms_since(t);
@@ -1252,8 +1290,17 @@ int plan_build(int device, int model, int64_t init_value, int n_hist, const int6
     msg = p->last_error;
     return rc;
   }
-  *out = p.release();
+  *out = reuse ? reuse : fresh.release();
   return 0;
+}
+
+// lc_check's plan per device, reused from call to call (buffers grow to the largest check);
+// guarded by the device mutex
+lc_plan* cached_plan(int dev) {
+  static std::unique_ptr<lc_plan> plans[64];
+  auto& c = plans[dev & 63];
+  if (!c) c.reset(new lc_plan());
+  return c.get();
 }
 
 bool valid_args(int model, int n_hist, const int64_t* hist_off, const int32_t* process,
@@ -1390,38 +1437,22 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
   int G = n_gpus <= 0 ? ndev : n_gpus;
   G = std::max(1, std::min(G, std::max(1, n_hist)));
 
-  // keep a copy for lc_failure_configs
+  // the caller's arrays, rebased to the first history (no copy)
+  const int64_t b0 = hist_off[0];
+  std::vector<int64_t> off0(hist_off, hist_off + n_hist + 1);
+  for (auto& x : off0) x -= b0;
+  auto at = [&](auto* ptr) { return ptr ? ptr + b0 : ptr; };
+  const int64_t* cidx = at(index);
+  const int32_t* cpr = at(process);
+  const int8_t *cty = at(type), *cf = at(f), *cvf = at(vflags);
+  const int64_t *cv0 = at(v0), *cv1 = at(v1);
   g_last = LastCheck();
-  g_last.model = model_kind;
-  g_last.init_value = init_value;
-  {
-    const int64_t n = hist_off[n_hist] - hist_off[0], b = hist_off[0];
-    g_last.off.assign(hist_off, hist_off + n_hist + 1);
-    for (auto& x : g_last.off) x -= b;
-    auto cp = [&](auto& dst, const auto* src) {
-      if (src) dst.assign(src + b, src + b + n);
-    };
-    cp(g_last.index, index);
-    cp(g_last.process, process);
-    cp(g_last.type, type);
-    cp(g_last.f, f);
-    cp(g_last.v0, v0);
-    cp(g_last.v1, v1);
-    cp(g_last.vflags, vflags);
-    if (!index) {  // :index defaults to the position within each history
-      g_last.index.resize(n);
-      for (int h = 0; h < n_hist; ++h)
-        for (int64_t i = g_last.off[h]; i < g_last.off[h + 1]; ++i) g_last.index[i] = i - g_last.off[h];
-    }
-  }
-  const LastCheck& L = g_last;
 
   // bounds pre-filter for counters (sound rejection only; never changes a verdict's index)
-  std::vector<int8_t> bounds_ok(n_hist, 1);
-  std::vector<int64_t> bounds_bad(n_hist, -1);
   if (model_kind == LC_MODEL_COUNTER && (flags & LC_FLAG_BOUNDS_ONLY)) {
-    int rc = lc_counter_bounds(init_value, n_hist, L.off.data(), L.index.data(), L.process.data(),
-                               L.type.data(), L.f.data(), L.v0.data(), L.v1.data(), L.vflags.data(),
+    std::vector<int8_t> bounds_ok(n_hist, 1);
+    std::vector<int64_t> bounds_bad(n_hist, -1);
+    int rc = lc_counter_bounds(init_value, n_hist, off0.data(), cidx, cpr, cty, cf, cv0, cv1, cvf,
                                bounds_ok.data(), bounds_bad.data(), err, err_len);
     if (rc) return rc;
     for (int h = 0; h < n_hist; ++h) {
@@ -1439,35 +1470,49 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
   std::vector<std::vector<int>> shard(G);
   {
     std::vector<int32_t> of(n_hist);
-    lpt_shards(n_hist, L.off.data(), G, of.data());
+    lpt_shards(n_hist, off0.data(), G, of.data());
     for (int h = 0; h < n_hist; ++h) shard[of[h]].push_back(h);
   }
   std::vector<int> rcs(G, 0);
   std::vector<std::string> msgs(G);
+  std::vector<int8_t> verdict(n_hist, LC_UNKNOWN);
   auto work = [&](int g) {
     const std::vector<int>& hs = shard[g];
     if (hs.empty()) return;
-    // gather this shard's histories into contiguous arrays
+    // this shard's histories as contiguous arrays: the caller's, in place, for one shard;
+    // else gathered (each history a contiguous run)
     std::vector<int64_t> off(1, 0), idx, a0, a1;
     std::vector<int32_t> pr;
     std::vector<int8_t> ty, ff, vf;
-    for (int h : hs) {
-      for (int64_t i = L.off[h]; i < L.off[h + 1]; ++i) {
-        idx.push_back(L.index[i]);
-        pr.push_back(L.process[i]);
-        ty.push_back(L.type[i]);
-        ff.push_back(L.f[i]);
-        a0.push_back(L.v0[i]);
-        a1.push_back(L.v1[i]);
-        vf.push_back(L.vflags[i]);
+    HistArrays a{off0[n_hist], cidx, cpr, cty, cf, cv0, cv1, cvf};
+    const int64_t* offp = off0.data();
+    if (G > 1) {
+      int64_t n = 0;
+      for (int h : hs) n += off0[h + 1] - off0[h];
+      if (cidx) idx.resize(n);
+      pr.resize(n), ty.resize(n), ff.resize(n), a0.resize(n), a1.resize(n), vf.resize(n);
+      int64_t o = 0;
+      for (int h : hs) {
+        const int64_t b = off0[h], m = off0[h + 1] - b;
+        if (cidx) std::copy_n(cidx + b, m, idx.data() + o);
+        std::copy_n(cpr + b, m, pr.data() + o);
+        std::copy_n(cty + b, m, ty.data() + o);
+        std::copy_n(cf + b, m, ff.data() + o);
+        std::copy_n(cv0 + b, m, a0.data() + o);
+        std::copy_n(cv1 + b, m, a1.data() + o);
+        std::copy_n(cvf + b, m, vf.data() + o);
+        o += m;
+        off.push_back(o);
       }
-      off.push_back((int64_t)idx.size());
+      a = HistArrays{n, cidx ? idx.data() : nullptr, pr.data(), ty.data(), ff.data(), a0.data(), a1.data(),
+                     vf.data()};
+      offp = off.data();
     }
     const int dev = g % ndev;
     std::lock_guard<std::mutex> lk(device_mutex(dev));
-    HistArrays a{off.back(), idx.data(), pr.data(), ty.data(), ff.data(), a0.data(), a1.data(), vf.data()};
     lc_plan* p = nullptr;
-    int rc = plan_build(dev, model_kind, init_value, (int)hs.size(), off.data(), a, max_configs, &p, msgs[g]);
+    int rc = plan_build(dev, model_kind, init_value, (int)hs.size(), offp, a, max_configs, &p, msgs[g],
+                        cached_plan(dev));
     if (!rc) {
       rc = p->run();
       if (rc) msgs[g] = p->last_error;
@@ -1480,6 +1525,7 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
       p->results(v.data(), fi.data(), fv.data(), po.data(), ex.data(), er.data());
       for (size_t k = 0; k < m; ++k) {
         const int h = hs[k];
+        verdict[h] = v[k];
         if (out_valid) out_valid[h] = v[k];
         if (out_fail_idx) out_fail_idx[h] = fi[k];
         if (out_fail_inv) out_fail_inv[h] = fv[k];
@@ -1488,11 +1534,7 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
         if (out_err) out_err[h] = er[k];
       }
     }
-    if (p) {
-      hipSetDevice(dev);
-      delete p;
-    }
-    rcs[g] = rc;
+    rcs[g] = rc;  // (p is the device's cached plan: kept for the next call)
   };
   if (G == 1) {
     work(0);
@@ -1506,7 +1548,27 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
       set_err(err, err_len, "shard %d (device %d): %s", g, g % ndev, msgs[g].c_str());
       return rcs[g];
     }
-  if (out_valid) g_last.valid.assign(out_valid, out_valid + n_hist);
+  // keep the invalid histories (only) for lc_failure_configs; the others get empty runs
+  g_last.model = model_kind;
+  g_last.init_value = init_value;
+  g_last.off.assign(n_hist + 1, 0);
+  for (int h = 0; h < n_hist; ++h)
+    g_last.off[h + 1] = g_last.off[h] + (verdict[h] == LC_INVALID ? off0[h + 1] - off0[h] : 0);
+  const int64_t nk = g_last.off[n_hist];
+  g_last.index.resize(nk), g_last.process.resize(nk), g_last.type.resize(nk), g_last.f.resize(nk);
+  g_last.v0.resize(nk), g_last.v1.resize(nk), g_last.vflags.resize(nk);
+  for (int h = 0; h < n_hist; ++h) {
+    if (verdict[h] != LC_INVALID) continue;
+    const int64_t sb = off0[h], m = off0[h + 1] - sb, o = g_last.off[h];
+    for (int64_t i = 0; i < m; ++i) g_last.index[o + i] = cidx ? cidx[sb + i] : i;  // :index or position
+    std::copy_n(cpr + sb, m, g_last.process.data() + o);
+    std::copy_n(cty + sb, m, g_last.type.data() + o);
+    std::copy_n(cf + sb, m, g_last.f.data() + o);
+    std::copy_n(cv0 + sb, m, g_last.v0.data() + o);
+    std::copy_n(cv1 + sb, m, g_last.v1.data() + o);
+    std::copy_n(cvf + sb, m, g_last.vflags.data() + o);
+  }
+  g_last.valid = verdict;
   g_last.have = true;
   return 0;
 }
@@ -1525,6 +1587,10 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
   const LastCheck& L = g_last;
   if (!L.have || hist < 0 || hist + 1 >= (int)L.off.size()) {
     set_err(err, err_len, "no checked history %d on this thread", hist);
+    return LC_E_ARG;
+  }
+  if (L.valid[hist] != LC_INVALID) {  // (only invalid histories are kept)
+    set_err(err, err_len, "history %d is not invalid", hist);
     return LC_E_ARG;
   }
   const int64_t b = L.off[hist], e = L.off[hist + 1];

@@ -17,7 +17,7 @@ from typing import Any, Dict, List, Optional, Sequence
 
 from . import _lib
 from . import history as H
-from .model import Model
+from .model import Inconsistent, Model, step
 
 VALID = {1: True, 0: False, 2: "unknown"}
 ERRORS = {0: None, -4: "malformed history", -5: "too many concurrently pending ops",
@@ -48,6 +48,61 @@ def _op_at(ops: List[Dict[str, Any]], index: int) -> Optional[Dict[str, Any]]:
     return ops[index] if 0 <= index < len(ops) else None
 
 
+def _folded_ops(ops) -> Dict[int, Dict[str, Any]]:
+    """invocation :index -> the op as the model steps it (knossos.history/complete [ext]: an
+    :ok completion's value folded into its invocation; :info keeps the invocation's)."""
+    by_proc: Dict[Any, Dict[str, Any]] = {}
+    out: Dict[int, Dict[str, Any]] = {}
+    for pos, o in enumerate(ops):
+        t = str(o.get("type", "")).lstrip(":")
+        idx = int(o.get("index", pos))
+        if t == "invoke":
+            op = {"index": idx, "process": o.get("process"), "f": str(o["f"]).lstrip(":"),
+                  "value": o.get("value")}
+            by_proc[o.get("process")] = op
+            out[idx] = op
+        elif o.get("process") in by_proc:
+            op = by_proc.pop(o.get("process"))
+            if t == "ok":
+                op["value"] = o.get("value")
+    return out
+
+
+def final_paths(model: Model, configs, pending, fail_inv: int, ops, k: int = 10):
+    """:final-paths of a Knossos failure report [ext] (jepsen.checker/linearizable keeps <= 10):
+    from each pre-failure config, sequences of pending ops linearized one after another, each
+    step consistent, ending with the failing op, whose step is inconsistent. Every config the
+    search reaches fails that op (that is why the verdict is false), so each path ends there.
+    Breadth-first (shortest paths first), pending ops in :index order. Each path is a list of
+    {"op", "model"}: the config's value first (op None), then every op with the value after it;
+    the last model is {"inconsistent": message}."""
+    folded = _folded_ops(ops)
+    fop = folded.get(fail_inv)
+    if fop is None:
+        return []
+    order = sorted(pending)
+    paths = []
+    queue = [((None if s is None else s) if model.name == "cas-register" else (s or 0),
+              frozenset(lin), [{"op": None, "model": {"value": s}}]) for (s, lin) in configs]
+    while queue and len(paths) < k:
+        nxt = []
+        for value, lin, path in queue:
+            r = step(model, value, fop["f"], fop["value"])
+            if isinstance(r, Inconsistent):
+                paths.append(path + [{"op": fop, "model": {"inconsistent": str(r)}}])
+                if len(paths) >= k:
+                    break
+            for i in order:
+                if i in lin or i == fail_inv or i not in folded:
+                    continue
+                o = folded[i]
+                r2 = step(model, value, o["f"], o["value"])
+                if not isinstance(r2, Inconsistent):
+                    nxt.append((r2, lin | {i}, path + [{"op": o, "model": {"value": r2}}]))
+        queue = nxt
+    return paths
+
+
 def _result_map(ops, r, k, model: Model, configs=None) -> Dict[str, Any]:
     v = VALID[int(r["valid"][k])]
     out: Dict[str, Any] = {"valid?": v, "analyzer": "linear",
@@ -58,12 +113,17 @@ def _result_map(ops, r, k, model: Model, configs=None) -> Dict[str, Any]:
     if v is False:
         out["op"] = _op_at(ops, int(r["fail_idx"][k]))
         out["previous-ok"] = _op_at(ops, int(r["prev_ok"][k]))
+        # :last-op, the op linearized last before the failure. JIT linearization stops a
+        # RETURN's closure at the returning op, so every config the previous RETURN produced
+        # linearized :previous-ok last (Knossos's README report shows them equal); configs
+        # carried through that RETURN unchanged keep an older last op. Unpinned vs Knossos.
         out["last-op"] = out["previous-ok"]
         out["invocation"] = _op_at(ops, int(r["fail_inv"][k]))
         if configs is not None:
             cfgs, pending = configs
             out["configs"] = [{"model": {"value": s}, "linearized": list(lin),
                                "pending": pending} for (s, lin) in cfgs]
+            out["final-paths"] = final_paths(model, cfgs, pending, int(r["fail_inv"][k]), ops)
     return out
 
 

@@ -34,3 +34,38 @@ def LeaderModel(state=None) -> Model:  # noqa: N802  (mirrors the Clojure record
     if state:
         raise ValueError("LeaderModel starts from the empty term map, as (LeaderModel. {}) does")
     return Model("leader", 0, 0, gpu=False)
+
+
+class Inconsistent(str):
+    """knossos.model/inconsistent [ext]: a step the model cannot take (its message)."""
+
+
+def step(model: Model, value, f: str, v):
+    """One model step on a plain value, for failure reports (the search itself runs on the
+    GPU). cas-register (knossos.model/CASRegister [ext]; register.clj:110): write v -> v;
+    cas [cur new] -> new iff cur = value; read v -> value iff v is nil or v = value.
+    CounterModel (counter.clj:100-127): add d -> value + d; decr d -> value - d; read x ->
+    value iff x nil or x = value; add-and-get [d n] -> n iff value + d = n (scalar d, the
+    :info case: value + d); decr-and-get mirrors it with -. Returns the new value or an
+    Inconsistent message."""
+    if model.name == "cas-register":
+        if f == "write":
+            return v
+        if f == "cas":
+            cur, new = v
+            return new if cur == value else Inconsistent(f"can't CAS {value} from {cur} to {new}")
+        if f == "read":
+            return value if v is None or v == value else Inconsistent(f"can't read {v} from register {value}")
+    elif model.name == "counter":
+        if f in ("add", "decr"):
+            return value + v if f == "add" else value - v
+        if f == "read":
+            return value if v is None or v == value else Inconsistent(f"can't read {v} from counter {value}")
+        if f in ("add-and-get", "decr-and-get"):
+            sign = 1 if f == "add-and-get" else -1
+            if isinstance(v, (list, tuple)):
+                d, n = v
+                return n if value + sign * d == n else Inconsistent(
+                    f"{'adding' if sign > 0 else 'decreasing'} {d} to {value} should result in {n}")
+            return value + sign * v
+    return Inconsistent(f"unknown :f {f} for {model.name}")

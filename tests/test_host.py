@@ -247,3 +247,67 @@ def test_independent_failures_exclude_unknown():
                 {"process": k, "type": "ok", "f": "read", "value": H.KV(k, k), "index": 2 * k + 1}]
     r = checker.independent_checker(Fixed()).check({}, ops)
     assert r["failures"] == [2] and r["valid?"] is False
+
+
+def _all_final_paths(model_name, cfgs, pending, fail_inv, ops, max_len):
+    """Independent enumeration (brute.step): every sequence of pending ops from a config,
+    each step consistent, ending with the failing op's inconsistent step (as op-index tuples)."""
+    import brute
+    folded = checker._folded_ops(ops)
+    fop = folded[fail_inv]
+    out = set()
+
+    def val(s):
+        return brute.NIL if s is None else s
+
+    def go(cfg, state, lin, seq):
+        if brute.step(model_name, state, fop["f"], fop["value"]) is None:
+            out.add((cfg,) + tuple(seq))
+        if len(seq) >= max_len:
+            return
+        for i in pending:
+            if i in lin or i == fail_inv or i not in folded:
+                continue
+            o = folded[i]
+            s2 = brute.step(model_name, state, o["f"], o["value"])
+            if s2 is not None:
+                go(cfg, s2, lin | {i}, seq + [i])
+    for c, (s, lin) in enumerate(cfgs):
+        go(c, val(s) if model_name == "cas-register" else s, frozenset(lin), [])
+    return out
+
+
+@pytest.mark.parametrize("model_name", ["cas-register", "counter"])
+def test_final_paths_against_enumeration(model_name):
+    """:final-paths: computed from the oracle's pre-failure configs, every
+    path is one the independent enumeration finds (compared as sets), each ends with the failing
+    op's inconsistent step, and the report holds min(10, all paths) of them, shortest first."""
+    m = model.cas_register() if model_name == "cas-register" else model.CounterModel(0)
+    gen = synth.gen_register if model_name == "cas-register" else synth.gen_counter
+    seen = 0
+    for t in range(40):
+        h = gen(60, 4, 0.1, 9000 + t, invalid=True)
+        e = oracle.check_one(model_name, h, with_configs=True)
+        if e["valid"] != 0:
+            continue
+        ops = h.to_ops(0)
+        cfgs = sorted(e["fail_configs"], key=lambda c: (c[0] is None, c[0] or 0, c[1]))[:10]
+        paths = checker.final_paths(m, cfgs, e["pending_inv_idx"], e["fail_inv_idx"], ops)
+        longest = max(len(p) for p in paths) - 2
+        every = _all_final_paths(model_name, cfgs, e["pending_inv_idx"], e["fail_inv_idx"], ops, longest)
+        got = set()
+        for p in paths:  # (config, ops...) - the config recovered from the path's first model
+            c = [i for i, (s_, lin) in enumerate(cfgs) if s_ == p[0]["model"]["value"]]
+            got.add(next((i,) + tuple(x["op"]["index"] for x in p[1:-1]) for i in c
+                         if (i,) + tuple(x["op"]["index"] for x in p[1:-1]) in every))
+        assert got <= every
+        assert len(paths) == min(10, len(_all_final_paths(model_name, cfgs, e["pending_inv_idx"],
+                                                          e["fail_inv_idx"], ops, longest + 1)))
+        for p in paths:
+            assert p[0]["op"] is None and "inconsistent" in p[-1]["model"]
+            assert p[-1]["op"]["index"] == e["fail_inv_idx"]
+            assert all("value" in s_["model"] for s_ in p[:-1])
+        # shortest first
+        assert [len(p) for p in paths] == sorted(len(p) for p in paths)
+        seen += 1
+    assert seen >= 3
