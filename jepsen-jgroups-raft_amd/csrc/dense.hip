@@ -395,8 +395,8 @@ struct StreamWin {
 __device__ __forceinline__ uint32_t read_step(const StreamWin& sw, int64_t pos, int lane, bool writer,
                                              OpSel* opt, int* ninv_out) {
   const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sw.at(pos));  // wave-uniform
-  const int ninv = (int)(H0 >> 27);
   const uint32_t w = sw.at(pos + 1 + lane);
+  const int ninv = (int)__builtin_ctzll(~__ballot(lane <= DENSE_MAX_NINV && (w & DENSE_OPW)));
   if (writer && lane < ninv) opt[w & 31u] = decode_op((w >> 8) & 0xffu, (w >> 16) & 0xffu);
   *ninv_out = ninv;
   return H0;
@@ -437,8 +437,8 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
       const uint32_t H0 = read_step(sw, pos, lane, tt < 64, opt, &ninv);
       pos += 1 + ninv;
       team_sync<TEAM>();
-      const uint32_t live = H0 & 0x3fffffu;
-      const int j = (int)((H0 >> 22) & 31u);
+      const uint32_t live = H0 & DENSE_LIVE_MASK;
+      const int j = (int)((H0 >> DENSE_J_SHIFT) & 31u);
       const uint32_t foldm = fold_mask(opt);
       const int Lw = 32 - __clz((int)live);
       const int nwt = 1 << (Lw > 3 ? Lw - 3 : 0);
@@ -504,7 +504,7 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
 // t-1's post-return frontier: zero means step t-1 is the failing RETURN. An empty frontier
 // stays empty, so the steps started after a failure add no explored configs.
 constexpr int PIPE_SERIAL_SEGS = DENSE_PIPE_SERIAL_SEGS;
-constexpr int PIPE_OPN = 24;  // op-table entries per step: OP_PAD + slots 0..16, + the pull batches' tail
+constexpr int PIPE_OPN = 26;  // op-table entries per step: OP_PAD + slots 0..24 (team slots), + the pull batches' tail
 struct __attribute__((aligned(16))) PipeStep {
   OpSel ops[PIPE_OPN];  // slot k at ops[OP_PAD + k]; every entry initialised
   uint32_t live, fresh, foldm, anyx;
@@ -521,8 +521,8 @@ __device__ __forceinline__ void pipe_decode(const DenseParams& p, StreamWin& sw,
                                             PipeStep* dst, const PipeStep* prev, uint32_t lmask = ~0u) {
   sw.need(p, pos, lane);
   const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sw.at(pos));
-  const int ninv = (int)(H0 >> 27);
   const uint32_t wd = sw.at(pos + 1 + lane);
+  const int ninv = (int)__builtin_ctzll(~__ballot(lane <= DENSE_MAX_NINV && (wd & DENSE_OPW)));
   const uint32_t plive = prev ? (uint32_t)rfl((int)prev->live) : 0u;
   const int pj = prev ? rfl(prev->j) : -1;
   if (lane < PIPE_OPN) dst->ops[lane] = prev ? prev->ops[lane] : OpSel{SEL_NONE, SEL_NONE};
@@ -531,13 +531,13 @@ __device__ __forceinline__ void pipe_decode(const DenseParams& p, StreamWin& sw,
   const uint32_t foldm =
       (uint32_t)__ballot(lane < PIPE_OPN - OP_PAD && dst->ops[OP_PAD + lane].hi == OPS_FOLD);
   if (lane == 0) {
-    const uint32_t live = H0 & 0x3fffffu, lloc = live & lmask;
+    const uint32_t live = H0 & DENSE_LIVE_MASK, lloc = live & lmask;
     const int L = lloc ? 32 - __clz((int)lloc) : 0;
     dst->live = live;
     dst->fresh = prev ? live & ~(plive & ~(1u << pj)) : live;
     dst->foldm = foldm;
     dst->anyx = 0;
-    dst->j = (int)((H0 >> 22) & 31u);
+    dst->j = (int)((H0 >> DENSE_J_SHIFT) & 31u);
     dst->jp = pj;
     dst->H = L > 3 ? L - 3 : 0;
     dst->start = 1 << 30;  // not started
@@ -1457,8 +1457,8 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     }
     uint64_t* const mine = mirror(rank);
     const uint32_t H0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.stream[hpos]);
-    const uint32_t live = H0 & 0x3fffffu;
-    const int j = (int)((H0 >> 22) & 31u);
+    const uint32_t live = H0 & DENSE_LIVE_MASK;
+    const int j = (int)((H0 >> DENSE_J_SHIFT) & 31u);
     const uint32_t foldm = fold_mask(sOp);
     const uint32_t live_loc = live & ((1u << lb) - 1), live_team = live >> lb;
     const bool active = ((uint32_t)rank & ~live_team) == 0;
@@ -1616,8 +1616,8 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
       const long long hpos = pos;
       pos += 1 + ninv;
       __syncthreads();
-      const uint32_t live = H0 & 0x3fffffu;
-      const int j = (int)((H0 >> 22) & 31u);
+      const uint32_t live = H0 & DENSE_LIVE_MASK;
+      const int j = (int)((H0 >> DENSE_J_SHIFT) & 31u);
       bool surv = false;
       if ((live >> lb) == 0) {  // narrow step: the leader alone (other tiles empty)
         if (rank == 0) {
@@ -1666,8 +1666,8 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
       const long long hpos = pos;
       pos += 1 + ninv;
       __syncthreads();
-      const uint32_t live = H0 & 0x3fffffu;
-      const int j = (int)((H0 >> 22) & 31u);
+      const uint32_t live = H0 & DENSE_LIVE_MASK;
+      const int j = (int)((H0 >> DENSE_J_SHIFT) & 31u);
       bool survived;
       if ((live >> lb) == 0) {  // narrow step: the leader alone (other tiles empty)
         const uint32_t foldm = fold_mask(sOp);

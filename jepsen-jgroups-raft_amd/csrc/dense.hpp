@@ -17,18 +17,23 @@ namespace lc {
 constexpr int DENSE_LMAX = 17;       // widest table a workgroup holds in LDS (128 KiB)
 constexpr int DENSE_WAVE_LMAX = 11;  // histories this narrow run one per wave
 constexpr int DENSE_MID_LMAX = 14;   // ... this narrow one per 256-thread workgroup (16 KiB table)
-constexpr int DENSE_WIDE_LMAX = 22;  // widest table a tile team holds (2^(22-17) LDS tiles)
+constexpr int DENSE_WIDE_LMAX = 24;  // widest history a tile team holds (<= 2^7 LDS tiles)
 constexpr int DENSE_MAX_STATES = 8;  // register values (state ids) per history
-constexpr int DENSE_WORD_BITS = DENSE_WIDE_LMAX - 3;  // bits of the sorted word list
+constexpr int DENSE_WORD_BITS = 19;  // bits of the sorted word list (a tile's words use <= 14)
+constexpr int DENSE_MAX_NINV = 30;   // invocations per step (a step must fit a 32-word window)
 constexpr int DENSE_MRING = 32;      // mirror slots per tile (pipelined tile teams)
 constexpr int DENSE_TEAM_MAXB = 7;   // team bits of a pipelined tile team (packed segments)
-constexpr int DENSE_TEAM_MAXB_SERIAL = DENSE_WIDE_LMAX - DENSE_LMAX;  // ... with serial segments
+constexpr int DENSE_TEAM_MAXB_SERIAL = 5;  // ... with serial segments
 constexpr int DENSE_PIPE_SERIAL_SEGS = 32;  // DenseParams.pipe bit 5: one pass per segment
 
 // Step stream (host-built, one u32 word stream per history):
-//   header  live[0:22) | j[22:27) | ninv[27:32)   live = pending slots after this step's
+//   header  live[0:24) | j[24:29), bit 31 clear   live = pending slots after this step's
 //                                                 invocations (includes the returning j)
-//   ninv op words: slot[0:8) | amask[8:16) | bmask[16:24)
+//   op words, one per invocation since the previous step (<= DENSE_MAX_NINV), bit 31 set:
+//           slot[0:8) | amask[8:16) | bmask[16:24) | DENSE_OPW
+//   (a decoder counts a step's op words with one ballot over the words that follow it)
+constexpr uint32_t DENSE_LIVE_MASK = 0xffffffu, DENSE_OPW = 1u << 31;
+constexpr int DENSE_J_SHIFT = 24;
 // register step on a state set S: x = S & amask; bmask ? (x ? bmask : 0) : x
 struct DenseParams {
   int32_t n;                    // histories in this launch (entries of order)

@@ -367,6 +367,8 @@ struct lc_plan {
     for (int h = 0; h < n; ++h) {
       ok[h] = !enc.err[h] && enc.n_states[h] <= DENSE_MAX_STATES && enc.live_max[h] <= dense_maxw;
       const int64_t s0 = enc.step_off[h], s1 = enc.step_off[h + 1];
+      for (int64_t g = s0; g < s1 && ok[h]; ++g)  // a step's words must fit the decoders' window
+        if (enc.inv_off[g + 1] - enc.inv_off[g] > DENSE_MAX_NINV) ok[h] = 0;
       dalg_off[h + 1] = dalg_off[h] + (ok[h] ? s1 - s0 : 0);
       wcount[h + 1] = wcount[h] + (ok[h] ? (s1 - s0) + (enc.inv_off[s1] - enc.inv_off[s0]) : 0);
     }
@@ -386,12 +388,12 @@ struct lc_plan {
         const int64_t q0 = enc.inv_off[g], q1 = enc.inv_off[g + 1];
         for (int64_t q = q0; q < q1; ++q) live |= 1u << enc.inv_slot[q];
         const uint32_t j = enc.step_slot[g];
-        *out++ = live | (j << 22) | ((uint32_t)(q1 - q0) << 27);
+        *out++ = live | (j << DENSE_J_SHIFT);
         for (int64_t q = q0; q < q1; ++q) {
           const int64_t a = enc.inv_a[q], b = enc.inv_b[q];
           const uint32_t am = a == R_ANY ? 0xffu : (a == R_NEVER ? 0u : (1u << a));
           const uint32_t bm = b < 0 ? 0u : (1u << b);
-          *out++ = (uint32_t)enc.inv_slot[q] | (am << 8) | (bm << 16);
+          *out++ = (uint32_t)enc.inv_slot[q] | (am << 8) | (bm << 16) | DENSE_OPW;
         }
         const int L = 32 - __builtin_clz(live);
         cost[h] += (double)(1u << L) * L;

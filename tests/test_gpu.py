@@ -110,10 +110,25 @@ def test_gpu_c2_full_size_vs_oracle():
 C4_EXPLORED = 10_994_841_001
 
 
-def test_gpu_c4_full_size_grid():
+def test_gpu_c4_full_size_grid(monkeypatch):
+    monkeypatch.setenv("LC_PATH", "grid")
     h = synth.gen_config("c4")
     assert h.n_ops() == 100_000
     g = _lib.check(1, 0, h)
+    assert int(g["err"][0]) == 0 and int(g["valid"][0]) == 1
+    assert int(g["explored"][0]) == C4_EXPLORED
+
+
+def test_gpu_c4_full_size_dense():
+    """C4 on the dense closure tables (the default path since steps carry 24 live slots): a
+    pipelined tile team of up to 2^7 workgroups; the same explored count as the grid kernel."""
+    h = synth.gen_config("c4")
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    g = p.results()
+    s = p.stats()
+    p.close()
+    assert s["dense_histories"] == 1
     assert int(g["err"][0]) == 0 and int(g["valid"][0]) == 1
     assert int(g["explored"][0]) == C4_EXPLORED
 
