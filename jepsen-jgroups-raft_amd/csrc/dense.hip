@@ -569,7 +569,7 @@ __device__ __forceinline__ T rdl(T v, int l) {
 template <int TEAM, int TLOG, int RING>
 __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, const uint64_t* zero,
                                              PipeStep* ring, int* sQ, unsigned long long* sExpl,
-                                             const uint32_t* words, const uint32_t* wofs, const uint32_t* binom,
+                                             const uint32_t* words_g, const uint32_t* wofs_g, const uint32_t* binom,
                                              int tt, unsigned long long& st_fout, unsigned long long& st_steps) {
   // pull batches read entries up to OP_PAD + b0 + 6 (b0 < H, a multiple of 4); slots < TLOG
   static_assert(OP_PAD + ((TLOG - 4) / 4) * 4 + 6 < PIPE_OPN && OP_PAD + TLOG <= PIPE_OPN, "op table too small");
@@ -591,6 +591,29 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
     const int NW = lmax > 3 ? 1 << (lmax - 3) : 1;
     const int ns = p.nsteps[h];
     for (int i = tt; i < NW; i += TEAM) B[i] = 0;
+    // a BLOCK history of width <= 16 leaves room in the LDS table for its own word list (the
+    // 2^(lmax-3) words below the table's width, by popcount layer) and the layers' offsets:
+    // the word index of a packed pass then comes from LDS, not from the global list
+    const uint32_t* words = words_g;
+    const uint32_t* wofs = wofs_g;
+    if constexpr (TLOG == DENSE_LMAX && TEAM >= 256) {
+      if (lmax <= DENSE_LMAX - 1 && lmax > 3) {
+        const int Hh = lmax - 3;
+        uint32_t* lw = reinterpret_cast<uint32_t*>(B + NW);
+        uint32_t* lo = lw + NW;
+        if (tt <= Hh + 1) {
+          uint32_t o = 0;
+          for (int q = 0; q < tt; ++q) o += binom[Hh * BINOM_N + q];
+          lo[tt] = o;
+        }
+        team_sync<TEAM>();
+        for (int q = 0; q <= Hh; ++q) {
+          const uint32_t nq = binom[Hh * BINOM_N + q], og = wofs_g[q], ol = lo[q];
+          for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)TEAM) lw[ol + r] = words_g[og + r];
+        }
+        words = lw, wofs = lo;
+      }
+    }
     team_sync<TEAM>();
     if (tt == 0) B[0] = 1;  // (cas-register) starts at nil: state id 0, nothing linearized
     StreamWin sw;
@@ -647,15 +670,13 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       uint64_t segm = __ballot(seg_l);
       mark(0);
       ++nsl;
-      if (!(p.pipe & PIPE_SERIAL_SEGS)) {
-        // packed: the running segments' words form one flat index f over the whole team
-        // (segment i = the ring lanes in order, its words at [e_i, e_i + nq_i)), so a
-        // super-layer of several small layers is ONE pass of every thread instead of one
-        // pass per segment; each thread reads its step's parameters from the ring in LDS
+      if (TEAM == 64 && !(p.pipe & PIPE_SERIAL_SEGS)) {
+        // one wave: the segments' words packed lane by lane (a wave team's layers are small),
+        // each lane with its own step's parameters from the ring entry
         uint32_t total = 0;
         for (uint64_t m = segm; m; m &= m - 1) total += rdl(nq_l, (int)__builtin_ctzll(m));
-        for (uint32_t f0 = 0; f0 < total; f0 += (uint32_t)TEAM) {
-          const uint32_t f = f0 + (uint32_t)tt;
+        for (uint32_t f0 = 0; f0 < total; f0 += 64u) {
+          const uint32_t f = f0 + (uint32_t)lane;
           int i = 0;
           uint32_t e = 0, acc = 0, o = 0;
           for (uint64_t m = segm; m; m &= m - 1) {
@@ -664,7 +685,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
             acc += rdl(nq_l, k);
           }
           if (f >= total) continue;
-          const uint32_t w = words[o + (f - e)];  // issued before the ring reads
+          const uint32_t w = words[o + (f - e)];
           const int t = t_ret_old + i;
           PipeStep* st = &ring[t % RING];
           const uint4 a = *reinterpret_cast<const uint4*>(&st->live);  // live, fresh, foldm, anyx
@@ -679,6 +700,45 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
           const uint64_t X = pipe_x(B, w, fresh >> 3, c.y, keep_lo);
           uint64_t R = pull_hi<4>(B, zero, w, c.x, c.z, ops, foldm);
           R = close_in_word(X, w, live, c.x, ops, foldm, R);
+          B[w] = X | R;
+          expl += (uint32_t)__popcll(R);
+          if (t > 0) st_fout += (uint32_t)__popcll(X);
+          if (X) st->anyx = 1;
+        }
+        segm = 0;
+      }
+      if (!(p.pipe & PIPE_SERIAL_SEGS)) {
+        // packed: the running segments' words form one flat index over the whole team, each
+        // segment padded to whole waves (segment i at [e_i, e_i + roundup(nq_i, 64))), so a
+        // super-layer of several small layers is ONE pass of the team instead of one pass per
+        // segment, and every wave works on a single step: its parameters are wave-uniform
+        // (readlanes of the ring view), its op branches scalar
+        uint32_t total = 0;
+        for (uint64_t m = segm; m; m &= m - 1) total += (rdl(nq_l, (int)__builtin_ctzll(m)) + 63u) & ~63u;
+        for (uint32_t f0 = (uint32_t)(tt & ~63); f0 < total; f0 += (uint32_t)TEAM) {
+          int i = 0;
+          uint32_t e = 0, acc = 0;
+          for (uint64_t m = segm; m; m &= m - 1) {
+            const int k = (int)__builtin_ctzll(m);
+            if (f0 >= acc) i = k, e = acc;
+            acc += (rdl(nq_l, k) + 63u) & ~63u;
+          }
+          const uint32_t nq = rdl(nq_l, i), r = f0 - e + (uint32_t)lane;
+          const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i), foldm = rdl(h0.z, i);
+          const int j = rdl(h1.x, i), jp = rdl(h1.y, i), H = rdl(h1.z, i);
+          const int t = t_ret_old + i;
+          if (r >= nq) continue;
+          const uint32_t w = words[rdl(o_l, i) + r];
+          if (w & ~(live >> 3)) continue;
+          uint64_t keep_lo = ~0ull;
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+            if (fresh & (1u << k)) keep_lo &= keep64(k);
+          PipeStep* st = &ring[t % RING];
+          const OpSel* ops = st->ops + OP_PAD;
+          const uint64_t X = pipe_x(B, w, fresh >> 3, jp, keep_lo);
+          uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+          R = close_in_word(X, w, live, j, ops, foldm, R);
           B[w] = X | R;
           expl += (uint32_t)__popcll(R);
           if (t > 0) st_fout += (uint32_t)__popcll(X);
@@ -1059,29 +1119,26 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     constexpr int TW = 2, TB = DENSE_TEAM_MAXB_SERIAL;
     if (!(p.pipe & PIPE_SERIAL_SEGS)) {
       constexpr int TB = DENSE_TEAM_MAXB;
-      // packed (as in history_pipe): one flat index over every running segment's words; each
-      // thread derives its step's parameters from the ring entry and this tile's rank
+      // packed (as in history_pipe): one flat index over every running segment's words, each
+      // segment padded to whole waves, so every wave works on one step with wave-uniform
+      // parameters (readlanes of the ring view and of this tile's per-segment values)
       uint32_t total = 0;
-      for (uint64_t m = segm; m; m &= m - 1) total += rdl(nq_l, (int)__builtin_ctzll(m));
-      for (uint32_t f0 = 0; f0 < total; f0 += 1024u) {
-        const uint32_t f = f0 + (uint32_t)tid;
+      for (uint64_t m = segm; m; m &= m - 1) total += (rdl(nq_l, (int)__builtin_ctzll(m)) + 63u) & ~63u;
+      for (uint32_t f0 = (uint32_t)(tid & ~63); f0 < total; f0 += 1024u) {
         int i = 0;
-        uint32_t e = 0, acc = 0, o = 0;
+        uint32_t e = 0, acc = 0;
         for (uint64_t m = segm; m; m &= m - 1) {
           const int k = (int)__builtin_ctzll(m);
-          if (f >= acc) i = k, e = acc, o = rdl(o_l, k);
-          acc += rdl(nq_l, k);
+          if (f0 >= acc) i = k, e = acc;
+          acc += (rdl(nq_l, k) + 63u) & ~63u;
         }
-        if (f >= total) continue;
-        const uint32_t w = p.words[o + (f - e)];  // issued before the ring reads
+        const uint32_t nq = rdl(nq_l, i), r = f0 - e + (uint32_t)lane;
+        const uint32_t mo = rdl(mo_l, i), mp = rdl(mp_l, i), pmask = rdl(pm_l, i), o = rdl(o_l, i);
+        const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i), foldm = rdl(h0.z, i);
+        const int j = rdl(h1.x, i), jp = rdl(h1.y, i), H = rdl(h1.z, i), xs = rdl(xs_l, i);
         const int t = t_ret_old + i;
-        PipeStep* st = &ring[t % RING];
-        const uint4 a = *reinterpret_cast<const uint4*>(&st->live);  // live, fresh, foldm, anyx
-        const int4 c = *reinterpret_cast<const int4*>(&st->j);       // j, jp, H, start
-        const int2 d = *reinterpret_cast<const int2*>(&st->pstart);  // pstart, hp
-        const uint32_t live = a.x, fresh = a.y, foldm = a.z;
-        const int j = c.x, jp = c.y, H = c.z, q = s - c.w;
-        const uint32_t r = f - e;
+        if (r >= nq) continue;
+        const uint32_t w = p.words[o + r];
         const uint32_t live_loc = live & lmask, lteam = live >> lb;
         if (w & ~(live_loc >> 3)) continue;
         const bool wide = lteam != 0;
@@ -1089,13 +1146,12 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
         const bool jloc_hi = j >= 3 && j < lb;
         const bool tile_fresh = ((uint32_t)rank & (fresh >> lb)) != 0;  // the tile's masks start empty
-        const uint32_t pmask = !wide ? 0u : tile_j ? (1u << jt) : ((uint32_t)rank & lteam);
-        const int xs = (jp >= lb && !tile_fresh) ? (rank | (1 << (jp - lb))) : -1;
         uint64_t keep_lo = ~0ull;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
           if (fresh & (1u << k)) keep_lo &= keep64(k);
         const uint32_t fresh_hi = (fresh & lmask) >> 3;
+        PipeStep* st = &ring[t % RING];
         const OpSel* ops = st->ops + OP_PAD;
         if (!wide && xs < 0) {  // a step on this tile alone (then tile 0, jp local): LDS only
           const uint64_t X = pipe_x(B, w, fresh_hi, jp, keep_lo);
@@ -1110,8 +1166,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         const bool fx = !tile_fresh && !(w & fresh_hi);
         // HBM loads first (X from tile xs, one pull per predecessor tile), used after
         uint64_t xv = 0, pv[TB];
-        if (fx && xs >= 0) xv = HbmTab::ld(mirror(xs, t - 1) + cum[d.y * BINOM_N + min(q, d.y)] + r);
-        const uint32_t mo = cum[H * BINOM_N + q];
+        if (fx && xs >= 0) xv = HbmTab::ld(mirror(xs, t - 1) + mp + r);
         // pulls from the tiles one team bit below: none for masks holding a local j (never
         // expanded); a tile holding j takes only T_j of r \ j
         const bool pl = tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u));
