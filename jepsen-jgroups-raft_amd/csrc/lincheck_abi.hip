@@ -135,7 +135,7 @@ struct lc_plan {
   std::vector<int64_t> dalg_off;    // [n_hist + 1] first step of each history in dalg
   int64_t dstream_words = 0;
   int dgrid_b = 0, dgrid_w = 0, dgrid_m = 0;
-  int tile_cap = 192, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
+  int tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
   int tile_lbits = DENSE_LMAX;                        // LC_TILE_LBITS: local slots per tile
   int wide_from = 99, wide_lbits = DENSE_LMAX;        // LC_TILE_WIDE=w:b: b local slots from width w
   // LC_PIPE: bits 0/1/2 = BLOCK/WAVE/TILE teams overlap steps (0: one at a time); bit 3 = tile
@@ -461,7 +461,7 @@ struct lc_plan {
     for (uint8_t L : ws) t += 4.67 + 0.00266 * std::ldexp(1.0, std::max(0, (int)L - 3));
     return t;
   }
-  double plan_k16 = 1.0;  // LC_PLAN_K: scales the team model's VALU term (calibration runs)
+  double plan_k16 = 1.3;  // LC_PLAN_K: scales the team model's VALU term (r2p sweep: 1.3 best on C3)
   double est_team_us(const std::vector<uint8_t>& ws, int lb) const {
     double t = 0;
     for (uint8_t L : ws) {
