@@ -33,6 +33,20 @@ MODEL_OF = {"c1": "cas-register", "c2": "cas-register", "c3": "cas-register",
             "c4": "cas-register", "c5": "counter"}
 
 
+# one process per GPU over RCCL ("nccl"); LC_BENCH_BACKEND=gloo and LC_BENCH_DEVICE=<index> are
+# test hooks that run several ranks on one GPU (the rank protocol, not the interconnect)
+BACKEND = os.environ.get("LC_BENCH_BACKEND", "nccl")
+
+
+def gpu_index() -> int:
+    d = os.environ.get("LC_BENCH_DEVICE")
+    return int(d) if d is not None else int(os.environ.get("LOCAL_RANK", 0))
+
+
+def coll_device() -> str:
+    return "cuda" if BACKEND == "nccl" else "cpu"
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -90,7 +104,7 @@ def bench_c5(args, rank, world, dist, barrier_sync):
     n = int(h.off[1] - h.off[0])
     own = shard.bounds_shard(n, rank, world)
     t0 = time.perf_counter()
-    plan = _lib.BoundsPlan(0, h, own=own, device=int(os.environ.get("LOCAL_RANK", 0)))
+    plan = _lib.BoundsPlan(0, h, own=own, device=gpu_index())
     log(f"[rank {rank}] c5: {n} entries, {h.n_ops()} ops, shard {own}; "
         f"plan {time.perf_counter() - t0:.2f}s")
 
@@ -112,7 +126,7 @@ def bench_c5(args, rank, world, dist, barrier_sync):
     elapsed = time.perf_counter() - t0
     if dist:
         torch, td = dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device())
         td.all_reduce(t, op=td.ReduceOp.MAX)
         elapsed = float(t.item())
     if rank != 0:
@@ -187,7 +201,7 @@ def bench_partition(args, rank, world, dist, barrier_sync):
     from lincheck import partition
     tdist = dist[1] if dist else None
     h = synth.gen_config(args.workload, scale=args.scale)
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = gpu_index()
     # per-rank lists of 2^cap configs; C4's widest closures need 2^25 on one rank
     cap = args.capacity_log2 or (25 if args.workload == "c4" else 22)
     runs = []
@@ -202,7 +216,7 @@ def bench_partition(args, rank, world, dist, barrier_sync):
     elapsed = time.perf_counter() - t0
     if dist:
         torch, td = dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device())
         td.all_reduce(t, op=td.ReduceOp.MAX)
         elapsed = float(t.item())
     if rank != 0:
@@ -302,13 +316,13 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = gpu_index()
     dist = None
     if world > 1:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group(BACKEND)
         dist = (torch, tdist)
 
     def barrier_sync():
@@ -364,7 +378,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         torch, tdist = dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device())
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     res = plan.results()
@@ -394,7 +408,7 @@ def main():
 
     if dist:
         # every rank's explored configs (the whole job's configs/s)
-        t = dist[0].tensor([explored_rank], dtype=dist[0].int64, device="cuda")
+        t = dist[0].tensor([explored_rank], dtype=dist[0].int64, device=coll_device())
         dist[1].all_reduce(t)
         explored_all = int(t.item())
     else:

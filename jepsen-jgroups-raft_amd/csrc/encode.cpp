@@ -46,23 +46,31 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
   std::vector<Op> ops;
   ops.reserve((size_t)(e - b) / 2 + 1);
   std::vector<int64_t> op_of(e - b, -1);
-  std::unordered_map<int32_t, int64_t> pend;
-  pend.reserve(64);
+  // process -> its outstanding op: open addressing over a power-of-two table (processes are
+  // arbitrary int32; a history has at most one per entry)
+  const size_t cap = (size_t)1 << (64 - __builtin_clzll((unsigned long long)(e - b) | 15));
+  std::vector<int32_t> pkey(cap * 2);
+  std::vector<int64_t> pval(cap * 2, -2);  // -2: empty slot, -1: no outstanding op
+  const size_t pmask = cap * 2 - 1;
+  auto slot_of = [&](int32_t proc) -> int64_t& {
+    size_t k = ((uint32_t)proc * 0x9E3779B1u) & pmask;
+    while (pval[k] != -2 && pkey[k] != proc) k = (k + 1) & pmask;
+    if (pval[k] == -2) pkey[k] = proc, pval[k] = -1;
+    return pval[k];
+  };
   for (int64_t i = b; i < e; ++i) {
     int8_t t = a.type[i];
-    auto it = pend.find(a.process[i]);
+    int64_t& cur = slot_of(a.process[i]);
     if (t == T_INVOKE) {
-      if (it != pend.end() && it->second >= 0)
-        return fail(LC_H_MALFORMED, "process invoked while an op was outstanding");
+      if (cur >= 0) return fail(LC_H_MALFORMED, "process invoked while an op was outstanding");
       Op op{i, -1, -1, a.f[i], a.vflags[i], a.v0[i], a.v1[i], -1};
-      pend[a.process[i]] = (int64_t)ops.size();
+      cur = (int64_t)ops.size();
       op_of[i - b] = (int64_t)ops.size();
       ops.push_back(op);
       o.n_ops++;
     } else if (t == T_OK || t == T_FAIL || t == T_INFO) {
-      if (it == pend.end() || it->second < 0)
-        return fail(LC_H_MALFORMED, "completion without an outstanding invocation");
-      Op& op = ops[it->second];
+      if (cur < 0) return fail(LC_H_MALFORMED, "completion without an outstanding invocation");
+      Op& op = ops[cur];
       op.cmp_pos = i;
       op.status = t;
       if (t == T_OK) {  // fold the completion's value into the invocation
@@ -70,21 +78,34 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
         op.v0 = a.v0[i];
         op.v1 = a.v1[i];
       }
-      op_of[i - b] = it->second;
-      it->second = -1;
+      op_of[i - b] = cur;
+      cur = -1;
     } else {
       return fail(LC_H_MALFORMED, "unknown :type");
     }
   }
 
-  // ---- model operands (memo for cas-register)
-  std::unordered_map<int64_t, int32_t> sid;  // value -> state id (id 0 = nil)
-  auto id_of = [&](int64_t v) -> int32_t {
+  // ---- model operands (memo for cas-register): value -> state id (id 0 = nil), ids in first-
+  // appearance order; a linear scan while the register has taken few values, then a map
+  std::unordered_map<int64_t, int32_t> sid;
+  auto find_id = [&](int64_t v) -> int32_t {  // 0 = not seen
+    if (o.state_val.size() <= 32) {
+      for (size_t k = 0; k < o.state_val.size(); ++k)
+        if (o.state_val[k] == v) return (int32_t)k + 1;
+      return 0;
+    }
     auto it = sid.find(v);
-    if (it != sid.end()) return it->second;
-    int32_t id = (int32_t)sid.size() + 1;
-    sid.emplace(v, id);
+    return it == sid.end() ? 0 : it->second;
+  };
+  auto id_of = [&](int64_t v) -> int32_t {
+    const int32_t f = find_id(v);
+    if (f) return f;
     o.state_val.push_back(v);
+    const int32_t id = (int32_t)o.state_val.size();
+    if (o.state_val.size() == 33)  // switch to the map: index every value seen so far
+      for (size_t k = 0; k < o.state_val.size(); ++k) sid.emplace(o.state_val[k], (int32_t)k + 1);
+    else if (o.state_val.size() > 33)
+      sid.emplace(v, id);
     return id;
   };
   std::vector<uint8_t> kind(ops.size(), 0);
@@ -100,19 +121,19 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
       const Op& op = ops[k];
       if (op.status == T_FAIL) continue;
       auto lookup = [&](int64_t v) -> int64_t {
-        auto it = sid.find(v);
-        return it == sid.end() ? R_NEVER : it->second;
+        const int32_t f = find_id(v);
+        return f ? f : R_NEVER;
       };
       switch (op.f) {
         case F_WRITE:  // write v -> v
           if (op.vflags == V_PAIR) return fail(LC_H_MODEL, "write with a pair value");
           opa[k] = R_ANY;
-          opb[k] = op.vflags == V_NIL ? 0 : sid[op.v0];
+          opb[k] = op.vflags == V_NIL ? 0 : find_id(op.v0);
           break;
         case F_CAS:  // cas [cur new] -> new iff cur = value
           if (op.vflags != V_PAIR) return fail(LC_H_MODEL, "cas without [cur new]");
           opa[k] = lookup(op.v0);
-          opb[k] = sid[op.v1];
+          opb[k] = find_id(op.v1);
           break;
         case F_READ:  // read v -> ok iff v nil or v = value
           if (op.vflags == V_PAIR) return fail(LC_H_MODEL, "read with a pair value");
@@ -123,7 +144,7 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
           return fail(LC_H_MODEL, "unknown :f for cas-register");
       }
     }
-    o.n_states = (int32_t)sid.size() + 1;
+    o.n_states = (int32_t)o.state_val.size() + 1;
     if (o.n_states > 65535) return fail(LC_H_WIDE, "more than 65535 distinct register values");
   } else {
     // CounterModel.step, counter.clj:102-127
@@ -205,17 +226,25 @@ void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
   out.init_value = init_value;
   std::vector<OneOut> parts(n_hist);
   int nt = (int)std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
-  if (hist_off[n_hist] < 200000) nt = 1;
-  std::vector<std::thread> th;
-  for (int w = 0; w < nt; ++w)
-    th.emplace_back([&, w] {
-      for (int h = w; h < n_hist; h += nt) encode_one(model, a, hist_off[h], hist_off[h + 1], parts[h]);
-    });
-  for (auto& t : th) t.join();
+  if (hist_off[n_hist] - hist_off[0] < 200000) nt = 1;
+  auto run = [&](auto&& fn) {  // fn(h) over every history, nt threads
+    std::vector<std::thread> th;
+    for (int w = 1; w < nt; ++w)
+      th.emplace_back([&, w] { for (int h = w; h < n_hist; h += nt) fn(h); });
+    for (int h = 0; h < n_hist; h += nt) fn(h);
+    for (auto& t : th) t.join();
+  };
+  run([&](int h) { encode_one(model, a, hist_off[h], hist_off[h + 1], parts[h]); });
 
+  // concatenate: offsets first, then every history's part copied in parallel
   out.step_off.assign(n_hist + 1, 0);
   out.state_off.assign(n_hist + 1, 0);
-  out.inv_off.push_back(0);
+  std::vector<int64_t> inv_base(n_hist + 1, 0);
+  out.err.resize(n_hist);
+  out.errmsg.resize(n_hist);
+  out.live_max.resize(n_hist);
+  out.n_states.resize(n_hist);
+  out.n_ops.resize(n_hist);
   for (int h = 0; h < n_hist; ++h) {
     OneOut& o = parts[h];
     if (o.err) {  // a failed history contributes no steps
@@ -223,30 +252,48 @@ void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
       o.step_ninv.clear();
       o.inv_slot.clear();
     }
-    out.err.push_back(o.err);
-    out.errmsg.push_back(o.msg);
-    out.live_max.push_back(o.live_max);
-    out.n_states.push_back(o.n_states);
-    out.n_ops.push_back(o.n_ops);
-    out.state_val.insert(out.state_val.end(), o.state_val.begin(), o.state_val.end());
-    out.state_off[h + 1] = (int64_t)out.state_val.size();
-    size_t inv_base = out.inv_slot.size();
+    out.err[h] = o.err;
+    out.errmsg[h] = std::move(o.msg);
+    out.live_max[h] = o.live_max;
+    out.n_states[h] = o.n_states;
+    out.n_ops[h] = o.n_ops;
+    out.step_off[h + 1] = out.step_off[h] + (int32_t)o.step_slot.size();
+    out.state_off[h + 1] = out.state_off[h] + (int64_t)o.state_val.size();
+    inv_base[h + 1] = inv_base[h] + (o.err ? 0 : (int64_t)o.inv_slot.size());
+  }
+  const int64_t ns = out.step_off[n_hist], ni = inv_base[n_hist];
+  out.state_val.resize(out.state_off[n_hist]);
+  out.step_slot.resize(ns);
+  out.step_cmp_idx.resize(ns);
+  out.step_inv_idx.resize(ns);
+  out.inv_off.resize(ns + 1);
+  out.inv_off[0] = 0;
+  out.inv_slot.resize(ni);
+  out.inv_kind.resize(ni);
+  out.inv_a.resize(ni);
+  out.inv_b.resize(ni);
+  out.inv_index.resize(ni);
+  run([&](int h) {
+    const OneOut& o = parts[h];
+    std::copy(o.state_val.begin(), o.state_val.end(), out.state_val.begin() + out.state_off[h]);
+    const int64_t s0 = out.step_off[h];
+    int64_t ib = inv_base[h];
     for (size_t s = 0; s < o.step_slot.size(); ++s) {
-      out.step_slot.push_back(o.step_slot[s]);
-      out.step_cmp_idx.push_back(o.step_cmp_idx[s]);
-      out.step_inv_idx.push_back(o.step_inv_idx[s]);
-      inv_base += (size_t)o.step_ninv[s];
-      out.inv_off.push_back((int64_t)inv_base);
+      out.step_slot[s0 + s] = o.step_slot[s];
+      out.step_cmp_idx[s0 + s] = o.step_cmp_idx[s];
+      out.step_inv_idx[s0 + s] = o.step_inv_idx[s];
+      ib += o.step_ninv[s];
+      out.inv_off[s0 + s + 1] = ib;
     }
     if (!o.err) {
-      out.inv_slot.insert(out.inv_slot.end(), o.inv_slot.begin(), o.inv_slot.end());
-      out.inv_kind.insert(out.inv_kind.end(), o.inv_kind.begin(), o.inv_kind.end());
-      out.inv_a.insert(out.inv_a.end(), o.inv_a.begin(), o.inv_a.end());
-      out.inv_b.insert(out.inv_b.end(), o.inv_b.begin(), o.inv_b.end());
-      out.inv_index.insert(out.inv_index.end(), o.inv_index.begin(), o.inv_index.end());
+      const int64_t q0 = inv_base[h];
+      std::copy(o.inv_slot.begin(), o.inv_slot.end(), out.inv_slot.begin() + q0);
+      std::copy(o.inv_kind.begin(), o.inv_kind.end(), out.inv_kind.begin() + q0);
+      std::copy(o.inv_a.begin(), o.inv_a.end(), out.inv_a.begin() + q0);
+      std::copy(o.inv_b.begin(), o.inv_b.end(), out.inv_b.begin() + q0);
+      std::copy(o.inv_index.begin(), o.inv_index.end(), out.inv_index.begin() + q0);
     }
-    out.step_off[h + 1] = (int32_t)out.step_slot.size();
-  }
+  });
 }
 
 }  // namespace lc

@@ -781,3 +781,36 @@ def test_gpu_recheck_stored_histories(tmp_path):
     rc = recheck.main([str(pc), "--workload", "counter"])
     ec = oracle.check_one("counter", c)
     assert rc == (0 if ec["valid"] == 1 else 1)
+
+
+# ---- the bench's multi-rank protocol (the driver runs it on 2/4/8 GPUs) -------------------
+
+@pytest.mark.parametrize("workload", ["c3", "c5"])
+def test_gpu_bench_two_ranks_one_gpu(workload, tmp_path):
+    """bench.py under torch.distributed.run with 2 ranks on cuda:0 (gloo; LC_BENCH_DEVICE=0):
+    C3's keys split over the ranks (lc_shard_histories), the max-over-ranks time, the summed
+    explored count; C5's scan shards with the 5-sum exchange. One JSON line, n_gpus = 2."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LC_BENCH_BACKEND="gloo", LC_BENCH_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--workload", workload]
+    if workload == "c3":
+        cmd += ["--scale", "0.2", "--e2e-reps", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["ms_per_step"] > 0
+    if workload == "c3":
+        assert out["config"]["histories"] == 200 and out["verdicts"]["0"] == 0
+        assert out["configs_explored_per_s"] > 0
+    else:
+        assert out["verdict"]["bounds_ok"] is True
