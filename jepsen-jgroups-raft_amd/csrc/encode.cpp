@@ -29,54 +29,123 @@ struct OneOut {
 };
 
 struct Op {
-  int64_t inv_pos, cmp_pos;
+  int64_t inv_pos;
+  int64_t v0, v1;
   int8_t status;  // -1 pending forever, else completion type
   int8_t f, vflags;
-  int64_t v0, v1;
-  int slot;
+  uint8_t slot;
 };
 
+// per-thread scratch, kept across histories (no allocation per history once warm)
+struct Scratch {
+  std::vector<Op> ops;
+  std::vector<int32_t> op_of;  // entry -> its op, -1 none
+  std::vector<int32_t> pkey;
+  std::vector<int32_t> pval;   // -2 empty slot, -1 no outstanding op, else op
+  std::unordered_map<int64_t, int32_t> sid;
+};
+
+// model operands of one op (cas-register: knossos.model/CASRegister [ext]; counter:
+// CounterModel.step, counter.clj:102-127); 0 or an LC_H_MODEL message
+template <class Find>
+const char* operands(int model, const Op& op, Find&& find_id, uint8_t& kind, int64_t& oa,
+                     int64_t& ob) {
+  kind = 0;
+  oa = ob = 0;
+  if (model == LC_MODEL_CAS_REGISTER) {
+    auto lookup = [&](int64_t v) -> int64_t {
+      const int32_t f = find_id(v);
+      return f ? f : R_NEVER;
+    };
+    switch (op.f) {
+      case F_WRITE:  // write v -> v
+        if (op.vflags == V_PAIR) return "write with a pair value";
+        oa = R_ANY;
+        ob = op.vflags == V_NIL ? 0 : find_id(op.v0);
+        return nullptr;
+      case F_CAS:  // cas [cur new] -> new iff cur = value
+        if (op.vflags != V_PAIR) return "cas without [cur new]";
+        oa = lookup(op.v0);
+        ob = find_id(op.v1);
+        return nullptr;
+      case F_READ:  // read v -> ok iff v nil or v = value
+        if (op.vflags == V_PAIR) return "read with a pair value";
+        oa = op.vflags == V_NIL ? R_ANY : lookup(op.v0);
+        ob = R_KEEP;
+        return nullptr;
+      default:
+        return "unknown :f for cas-register";
+    }
+  }
+  switch (op.f) {
+    case F_ADD:
+    case F_DECR:
+      if (op.vflags != V_SCALAR) return ":add/:decr need a scalar delta";
+      kind = op.f == F_DECR ? C_SUB : 0;
+      ob = op.v0;
+      return nullptr;
+    case F_READ:
+      if (op.vflags == V_PAIR) return ":read with a pair value";
+      kind = op.vflags == V_NIL ? 0 : C_PRE_EQ;
+      oa = op.v0;
+      return nullptr;
+    case F_AAG:
+    case F_DAG:
+      if (op.vflags == V_NIL) return "*-and-get without a delta";
+      kind = (op.f == F_DAG ? C_SUB : 0) | (op.vflags == V_PAIR ? C_POST_EQ : 0);
+      ob = op.v0;
+      oa = op.vflags == V_PAIR ? op.v1 : 0;
+      return nullptr;
+    default:
+      return "unknown :f for CounterModel";
+  }
+}
+
 void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o) {
+  thread_local Scratch sc;
   auto IDX = [&](int64_t pos) { return a.index ? a.index[pos] : pos - b; };
+  std::vector<Op>& ops = sc.ops;
   auto fail = [&](int code, const char* m) {
     o.err = code;
     o.msg = m;
+    o.n_ops = (int64_t)ops.size();
   };
   // ---- pairing (knossos.history [ext])
-  std::vector<Op> ops;
-  ops.reserve((size_t)(e - b) / 2 + 1);
-  std::vector<int64_t> op_of(e - b, -1);
+  ops.clear();
+  std::vector<int32_t>& op_of = sc.op_of;
+  op_of.assign(e - b, -1);
   // process -> its outstanding op: open addressing over a power-of-two table (processes are
   // arbitrary int32; a history has at most one per entry)
   const size_t cap = (size_t)1 << (64 - __builtin_clzll((unsigned long long)(e - b) | 15));
-  std::vector<int32_t> pkey(cap * 2);
-  std::vector<int64_t> pval(cap * 2, -2);  // -2: empty slot, -1: no outstanding op
   const size_t pmask = cap * 2 - 1;
-  auto slot_of = [&](int32_t proc) -> int64_t& {
+  sc.pkey.resize(cap * 2);
+  sc.pval.assign(cap * 2, -2);
+  int32_t* pkey = sc.pkey.data();
+  int32_t* pval = sc.pval.data();
+  auto slot_of = [&](int32_t proc) -> int32_t& {
     size_t k = ((uint32_t)proc * 0x9E3779B1u) & pmask;
     while (pval[k] != -2 && pkey[k] != proc) k = (k + 1) & pmask;
     if (pval[k] == -2) pkey[k] = proc, pval[k] = -1;
     return pval[k];
   };
+  int64_t n_ok = 0;
   for (int64_t i = b; i < e; ++i) {
     int8_t t = a.type[i];
-    int64_t& cur = slot_of(a.process[i]);
+    int32_t& cur = slot_of(a.process[i]);
     if (t == T_INVOKE) {
       if (cur >= 0) return fail(LC_H_MALFORMED, "process invoked while an op was outstanding");
-      Op op{i, -1, -1, a.f[i], a.vflags[i], a.v0[i], a.v1[i], -1};
-      cur = (int64_t)ops.size();
-      op_of[i - b] = (int64_t)ops.size();
-      ops.push_back(op);
-      o.n_ops++;
+      cur = (int32_t)ops.size();
+      op_of[i - b] = cur;
+      ops.push_back(Op{i, a.v0[i], a.v1[i], -1, a.f[i], a.vflags[i], 0});
     } else if (t == T_OK || t == T_FAIL || t == T_INFO) {
       if (cur < 0) return fail(LC_H_MALFORMED, "completion without an outstanding invocation");
       Op& op = ops[cur];
-      op.cmp_pos = i;
       op.status = t;
       if (t == T_OK) {  // fold the completion's value into the invocation
         op.vflags = a.vflags[i];
         op.v0 = a.v0[i];
         op.v1 = a.v1[i];
+        n_ok++;
       }
       op_of[i - b] = cur;
       cur = -1;
@@ -84,10 +153,11 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
       return fail(LC_H_MALFORMED, "unknown :type");
     }
   }
-
-  // ---- model operands (memo for cas-register): value -> state id (id 0 = nil), ids in first-
-  // appearance order; a linear scan while the register has taken few values, then a map
-  std::unordered_map<int64_t, int32_t> sid;
+  o.n_ops = (int64_t)ops.size();
+  // ---- cas-register memo: value -> state id (id 0 = nil), ids in first-appearance order over
+  // the values the register can hold; a linear scan while it has taken few values, then a map
+  std::unordered_map<int64_t, int32_t>& sid = sc.sid;
+  sid.clear();
   auto find_id = [&](int64_t v) -> int32_t {  // 0 = not seen
     if (o.state_val.size() <= 32) {
       for (size_t k = 0; k < o.state_val.size(); ++k)
@@ -97,109 +167,67 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
     auto it = sid.find(v);
     return it == sid.end() ? 0 : it->second;
   };
-  auto id_of = [&](int64_t v) -> int32_t {
-    const int32_t f = find_id(v);
-    if (f) return f;
-    o.state_val.push_back(v);
-    const int32_t id = (int32_t)o.state_val.size();
-    if (o.state_val.size() == 33)  // switch to the map: index every value seen so far
-      for (size_t k = 0; k < o.state_val.size(); ++k) sid.emplace(o.state_val[k], (int32_t)k + 1);
-    else if (o.state_val.size() > 33)
-      sid.emplace(v, id);
-    return id;
-  };
-  std::vector<uint8_t> kind(ops.size(), 0);
-  std::vector<int64_t> opa(ops.size(), 0), opb(ops.size(), 0);
   if (model == LC_MODEL_CAS_REGISTER) {
-    // pass 1: values the register can hold (knossos.model/CASRegister [ext])
-    for (auto& op : ops) {
+    for (const Op& op : ops) {
       if (op.status == T_FAIL) continue;
-      if (op.f == F_WRITE && op.vflags == V_SCALAR) id_of(op.v0);
-      if (op.f == F_CAS && op.vflags == V_PAIR) id_of(op.v1);
-    }
-    for (size_t k = 0; k < ops.size(); ++k) {
-      const Op& op = ops[k];
-      if (op.status == T_FAIL) continue;
-      auto lookup = [&](int64_t v) -> int64_t {
-        const int32_t f = find_id(v);
-        return f ? f : R_NEVER;
-      };
-      switch (op.f) {
-        case F_WRITE:  // write v -> v
-          if (op.vflags == V_PAIR) return fail(LC_H_MODEL, "write with a pair value");
-          opa[k] = R_ANY;
-          opb[k] = op.vflags == V_NIL ? 0 : find_id(op.v0);
-          break;
-        case F_CAS:  // cas [cur new] -> new iff cur = value
-          if (op.vflags != V_PAIR) return fail(LC_H_MODEL, "cas without [cur new]");
-          opa[k] = lookup(op.v0);
-          opb[k] = find_id(op.v1);
-          break;
-        case F_READ:  // read v -> ok iff v nil or v = value
-          if (op.vflags == V_PAIR) return fail(LC_H_MODEL, "read with a pair value");
-          opa[k] = op.vflags == V_NIL ? R_ANY : lookup(op.v0);
-          opb[k] = R_KEEP;
-          break;
-        default:
-          return fail(LC_H_MODEL, "unknown :f for cas-register");
-      }
-    }
-    o.n_states = (int32_t)o.state_val.size() + 1;
-    if (o.n_states > 65535) return fail(LC_H_WIDE, "more than 65535 distinct register values");
-  } else {
-    // CounterModel.step, counter.clj:102-127
-    for (size_t k = 0; k < ops.size(); ++k) {
-      const Op& op = ops[k];
-      if (op.status == T_FAIL) continue;
-      switch (op.f) {
-        case F_ADD:
-        case F_DECR:
-          if (op.vflags != V_SCALAR) return fail(LC_H_MODEL, ":add/:decr need a scalar delta");
-          kind[k] = op.f == F_DECR ? C_SUB : 0;
-          opb[k] = op.v0;
-          break;
-        case F_READ:
-          if (op.vflags == V_PAIR) return fail(LC_H_MODEL, ":read with a pair value");
-          kind[k] = op.vflags == V_NIL ? 0 : C_PRE_EQ;
-          opa[k] = op.v0;
-          opb[k] = 0;
-          break;
-        case F_AAG:
-        case F_DAG:
-          if (op.vflags == V_NIL) return fail(LC_H_MODEL, "*-and-get without a delta");
-          kind[k] = (op.f == F_DAG ? C_SUB : 0) | (op.vflags == V_PAIR ? C_POST_EQ : 0);
-          opb[k] = op.v0;
-          opa[k] = op.vflags == V_PAIR ? op.v1 : 0;
-          break;
-        default:
-          return fail(LC_H_MODEL, "unknown :f for CounterModel");
-      }
+      int64_t v;
+      if (op.f == F_WRITE && op.vflags == V_SCALAR) v = op.v0;
+      else if (op.f == F_CAS && op.vflags == V_PAIR) v = op.v1;
+      else continue;
+      if (find_id(v)) continue;
+      o.state_val.push_back(v);
+      if (o.state_val.size() == 33)  // switch to the map: index every value seen so far
+        for (size_t k = 0; k < o.state_val.size(); ++k) sid.emplace(o.state_val[k], (int32_t)k + 1);
+      else if (o.state_val.size() > 33)
+        sid.emplace(v, (int32_t)o.state_val.size());
     }
   }
 
-  // ---- RETURN steps with slot assignment (lowest free slot first)
+  // ---- RETURN steps with slot assignment (lowest free slot first), operands computed at each
+  // invocation. Error precedence: a model error anywhere, then > 65535 register values, then
+  // > 63 pending ops.
+  o.step_slot.reserve(n_ok);
+  o.step_ninv.reserve(n_ok);
+  o.step_cmp_idx.reserve(n_ok);
+  o.step_inv_idx.reserve(n_ok);
+  o.inv_slot.reserve(ops.size());
+  o.inv_kind.reserve(ops.size());
+  o.inv_a.reserve(ops.size());
+  o.inv_b.reserve(ops.size());
+  o.inv_index.reserve(ops.size());
+  const char* wide = nullptr;
   uint64_t used = 0;
   int64_t ninv_cur = 0;
   for (int64_t i = b; i < e; ++i) {
-    int64_t k = op_of[i - b];
+    const int32_t k = op_of[i - b];
     if (k < 0) continue;
     Op& op = ops[k];
-    int8_t t = a.type[i];
+    const int8_t t = a.type[i];
     if (t == T_INVOKE) {
       if (op.status == T_FAIL) continue;  // failed ops never enter the search
-      if (used == ~0ull >> (64 - MAX_SLOTS)) return fail(LC_H_WIDE, "more than 63 pending ops");
-      int s = __builtin_ctzll(~used);
+      uint8_t kind;
+      int64_t oa, ob;
+      if (const char* m = operands(model, op, find_id, kind, oa, ob)) {
+        o.live_max = 0;
+        return fail(LC_H_MODEL, m);
+      }
+      if (wide) continue;  // only model errors are still looked for
+      if (used == ~0ull >> (64 - MAX_SLOTS)) {
+        wide = "more than 63 pending ops";
+        continue;
+      }
+      const int s = __builtin_ctzll(~used);
       used |= 1ull << s;
-      op.slot = s;
+      op.slot = (uint8_t)s;
       o.live_max = std::max(o.live_max, 64 - __builtin_clzll(used));
       o.inv_slot.push_back((uint8_t)s);
-      o.inv_kind.push_back(kind[k]);
-      o.inv_a.push_back(opa[k]);
-      o.inv_b.push_back(opb[k]);
+      o.inv_kind.push_back(kind);
+      o.inv_a.push_back(oa);
+      o.inv_b.push_back(ob);
       o.inv_index.push_back(IDX(op.inv_pos));
       ninv_cur++;
-    } else if (t == T_OK) {
-      o.step_slot.push_back((uint8_t)op.slot);
+    } else if (t == T_OK && !wide) {
+      o.step_slot.push_back(op.slot);
       o.step_ninv.push_back(ninv_cur);
       o.step_cmp_idx.push_back(IDX(i));
       o.step_inv_idx.push_back(IDX(op.inv_pos));
@@ -207,6 +235,14 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
       used &= ~(1ull << op.slot);
     }
   }
+  if (model == LC_MODEL_CAS_REGISTER) {
+    o.n_states = (int32_t)o.state_val.size() + 1;
+    if (o.n_states > 65535) {
+      o.live_max = 0;
+      return fail(LC_H_WIDE, "more than 65535 distinct register values");
+    }
+  }
+  if (wide) return fail(LC_H_WIDE, wide);
   // invocations after the last RETURN never matter: drop them
   size_t keep = o.inv_slot.size() - (size_t)ninv_cur;
   o.inv_slot.resize(keep);
