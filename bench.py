@@ -209,7 +209,8 @@ def bench_partition(args, rank, world, dist, barrier_sync):
         if i == args.warmup:
             barrier_sync()
             t0 = time.perf_counter()
-        r = partition.check_partitioned(h, tdist=tdist, device_index=local, capacity_log2=cap)
+        r = partition.check_partitioned(h, tdist=tdist, device_index=local, capacity_log2=cap,
+                                        device_loop=not args.level_protocol)
         if i >= args.warmup:
             runs.append(r)
     barrier_sync()
@@ -222,6 +223,7 @@ def bench_partition(args, rank, world, dist, barrier_sync):
     if rank != 0:
         return None
     r = runs[-1]
+    dev_loop = world == 1 and not args.level_protocol
     k_s = sum(x["kernel_ms"] for x in runs) / len(runs) / 1e3
     achieved = r["alg_bytes"] / k_s / 1e9 if k_s > 0 else 0.0
     return {
@@ -240,16 +242,21 @@ def bench_partition(args, rank, world, dist, barrier_sync):
         "config": {"workload": f"{args.workload}: one register history, frontier partitioned "
                                f"by config hash over {world} rank(s)",
                    "ops": h.n_ops(), "scale": args.scale,
-                   "parallelism": f"axis 2: {world} GPU(s), one all-to-all per BFS level"},
+                   "parallelism": f"axis 2: {world} GPU(s), " + (
+                       "device-resident level loop (lc_part_run)" if dev_loop else
+                       "one all-to-all per BFS level")},
         "configs_explored_per_s": r["explored"] * args.steps / elapsed,
         "verdict": {"valid": r["valid"], "explored": r["explored"], "steps": r["steps"],
                     "levels": r["levels"], "exchanged_bytes": r["exchanged_bytes"]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "lc::part_expand + lc::part_absorb (rank 0)",
+                     "kernel": "lc::part_step_kernel" if dev_loop else
+                               "lc::part_expand + lc::part_absorb (rank 0)",
                      "kernel_ms": k_s * 1e3, "alg_bytes_per_launch": r["alg_bytes"],
-                     "note": "per check (all levels); the wall time is dominated by the per-level "
-                             "host round trip (count exchange + all-to-all), see DESIGN.md §6"},
+                     "note": "per check (all levels); " + (
+                         "GPU time from the first step's launch to the last one's end" if dev_loop
+                         else "the wall time is dominated by the per-level host round trip "
+                              "(count exchange + all-to-all), see DESIGN.md §6")},
         "cpu_baseline": None,
     }
 
@@ -310,6 +317,8 @@ def main():
     ap.add_argument("--partition", action="store_true",
                     help="axis 2: one history (c2/c4) with its frontier partitioned over ranks")
     ap.add_argument("--capacity-log2", type=int, default=0, help="--partition: per-rank capacity")
+    ap.add_argument("--level-protocol", action="store_true",
+                    help="--partition at 1 GPU: the host-driven level protocol, not lc_part_run")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC passes (or absent)")
     args = ap.parse_args()

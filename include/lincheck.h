@@ -214,6 +214,15 @@ int32_t lc_part_step_end(lc_part* p, void* stream, int64_t* out_count, char* err
  * invocation, [3] of step t-1's completion (-1 at t = 0) */
 int32_t lc_part_results(lc_part* p, int64_t t, void* stream, int64_t* out4, char* err,
                         int32_t err_len);
+/* World 1, device-resident (no host round trip per level): runs the steps of a fresh plan to
+ * the end, to max_steps (< 0: all) or to the first failing step, one cooperative launch per
+ * step whose workgroups loop over its BFS levels behind grid barriers, each level absorbing
+ * its candidates and expanding the new configs at once. Same verdict, failing step and
+ * explored count as the step_begin/expand/absorb/step_end protocol (which world > 1 uses).
+ * out4[0] steps run, [1] first failing step (-1: none), [2] BFS levels, [3] explored.
+ * lc_part_results reads the failing step's :index triple afterwards. */
+int32_t lc_part_run(lc_part* p, void* stream, int64_t max_steps, int64_t* out4, char* err,
+                    int32_t err_len);
 void lc_part_destroy(lc_part* p);
 
 #ifdef __cplusplus

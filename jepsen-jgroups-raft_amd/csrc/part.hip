@@ -45,16 +45,26 @@ constexpr uint64_t DIRECT = 1ull << 63;      // in transit: already returned, go
 constexpr int PT = 256;                      // threads per workgroup
 constexpr uint32_t EPOCH_MAX = 0xffffu;
 
-enum : int { PF_OVERFLOW = 1 };
+enum : int { PF_OVERFLOW = 1, PF_STAGE = 2, PF_ABORT = 4 };
 
-// device counters of one rank (one D2H read per level)
+// device counters of one rank (one D2H read per level; per chunk of steps in lc_part_run)
 struct PartCtl {
   unsigned long long cnt[PW_MAX];  // candidates per destination (this level)
   unsigned long long lc[2];        // level lists (count)
   unsigned long long oc[2];        // frontier F / OUT list, by step parity (F = oc[sp ^ 1])
   unsigned long long explored;     // all steps
   unsigned long long flags;
-  unsigned long long pad[6];
+  unsigned long long lvl[3];       // lc_part_run: candidates of level l in lvl[l % 3]
+  unsigned long long listed;       // lc_part_run: configs expanded, candidates absorbed,
+  unsigned long long cand;         //   BFS levels (for the algorithmic bytes / stats)
+  unsigned long long levels;
+};
+
+// lc_part_run's grid barrier words, each on its own 64-B line
+struct PartBar {
+  unsigned grp[8][16];
+  unsigned top, pad0[15];
+  unsigned gen, pad1[15];
 };
 
 struct StepArgs {
@@ -268,6 +278,212 @@ __global__ void __launch_bounds__(PT) part_absorb(const uint64_t* __restrict__ r
   if (__lane_id() == 0 && expl) atomicAdd(&ctl->explored, expl);
 }
 
+// ---- lc_part_run (world 1): one cooperative launch per RETURN step runs all of its levels,
+// separated by grid barriers; a level absorbs its candidates and expands the new configs at
+// once (no level list, no host round trip). The host reads the per-step OUT counts once per
+// chunk of steps.
+constexpr int PL = 512;  // threads per workgroup
+constexpr int PLW = PL / 64;
+constexpr int PAB = 4;   // candidates per thread per pass
+
+struct RunArgs {
+  uint64_t* S;
+  uint64_t* O;
+  uint64_t tmask;
+  const uint64_t* F;
+  uint64_t* outl;
+  uint64_t list_cap;
+  uint64_t* stage[2];
+  uint64_t seg_cap;
+  PartCtl* ctl;
+  PartBar* bar;
+  unsigned long long* flog;  // OUT count per step of the chunk
+  uint32_t flog_i;
+  int32_t sp;
+  uint64_t ep;
+  uint32_t wd, nwg;
+};
+
+// Grid barrier: 8 group counters then a top counter, release generation polled relaxed with
+// s_sleep (MI355X_MICROARCH "barrier-xcd"); the data a level hands on is sc1 stores and
+// device-scope atomics, read back with sc1 loads. A 20 s watchdog raises PF_ABORT.
+__device__ __forceinline__ bool run_sync(const RunArgs& r, int* s_abort) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    PartBar* bar = r.bar;
+    const unsigned g = ld_agent(&bar->gen);
+    const unsigned grp = blockIdx.x & 7u;
+    const unsigned gsize = (r.nwg - grp + 7u) >> 3;
+    const unsigned ngroups = r.nwg < 8u ? r.nwg : 8u;
+    const unsigned a = __hip_atomic_fetch_add(&bar->grp[grp][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a == gsize - 1) {
+      st_agent(&bar->grp[grp][0], 0u);
+      const unsigned t = __hip_atomic_fetch_add(&bar->top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == ngroups - 1) {
+        st_agent(&bar->top, 0u);
+        __hip_atomic_store(&bar->gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    long spins = 0;
+    while (ld_agent(&bar->gen) == g) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+          atomicOr(&r.ctl->flags, (unsigned long long)PF_ABORT);
+          break;
+        }
+        if (ld_agent(&r.ctl->flags) & PF_ABORT) break;
+      }
+    }
+    *s_abort = (ld_agent(&r.ctl->flags) & PF_ABORT) != 0;
+  }
+  __syncthreads();
+  return *s_abort == 0;
+}
+
+// Every thread's candidates from its NU configs (ok[u]) appended to dst at positions reserved
+// with one wave scan, one block prefix and one global atomic per block. Block-uniform call.
+template <int NU>
+__device__ __forceinline__ void emit(const StepArgs& a, const uint64_t* c, const bool* ok, uint32_t wd,
+                                     uint64_t mmask, uint64_t* dst, uint64_t cap, unsigned long long* counter,
+                                     PartCtl* ctl, uint32_t* s_w, unsigned long long* s_base) {
+  uint32_t tc = 0;
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+    if (ok[u])
+      for (int k = 0; k < (int)wd; ++k) tc += candidate(a, c[u], true, k, mmask).has;
+  const int lane = __lane_id(), w = threadIdx.x >> 6;
+  uint32_t x = tc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t sum = 0;
+    for (int i = 0; i < PLW; ++i) {
+      const uint32_t v = s_w[i];
+      s_w[i] = sum;
+      sum += v;
+    }
+    *s_base = sum ? atomicAdd(counter, (unsigned long long)sum) : 0ull;
+  }
+  __syncthreads();
+  uint64_t pos = *s_base + s_w[w] + (x - tc);
+  bool over = false;
+  if (tc) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      if (ok[u])
+        for (int k = 0; k < (int)wd; ++k) {
+          const Cand q = candidate(a, c[u], true, k, mmask);
+          if (!q.has) continue;
+          if (pos < cap) st_agent(&dst[pos], q.out);
+          else over = true;
+          ++pos;
+        }
+  }
+  if (over) atomicOr(&ctl->flags, (unsigned long long)PF_STAGE);
+  __syncthreads();  // s_w / s_base are reused
+}
+
+__global__ void __launch_bounds__(PL) part_step_kernel(StepArgs a, RunArgs r) {
+  __shared__ uint32_t s_w[PLW];
+  __shared__ unsigned long long s_base;
+  __shared__ int s_abort;
+  PartCtl* ctl = r.ctl;
+  const uint64_t mmask = (1ull << a.mask_bits) - 1;
+  unsigned long long* out_count = &ctl->oc[r.sp];
+  const int tid = threadIdx.x, lane = __lane_id();
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  // level 0: expand the frontier into stage 0
+  if (lead) st_agent(out_count, 0ull);
+  const uint64_t nf = ld_agent(&ctl->oc[r.sp ^ 1]);
+  const uint64_t stride = (uint64_t)r.nwg * PL;
+  for (uint64_t it = (uint64_t)blockIdx.x * PL; it < nf; it += stride) {  // block-uniform trip count
+    const uint64_t i = it + tid;
+    const bool ok = i < nf;
+    const uint64_t c = ok ? r.F[i] : 0ull;
+    emit<1>(a, &c, &ok, r.wd, mmask, r.stage[0], r.seg_cap, &ctl->lvl[0], ctl, s_w, &s_base);
+  }
+  if (!run_sync(r, &s_abort)) return;
+  unsigned long long expl = 0, listed = 0;
+  int l = 0;
+  for (;; ++l) {
+    const uint64_t n_raw = ld_agent(&ctl->lvl[l % 3]);
+    if (n_raw == 0) break;
+    const uint64_t n = n_raw < r.seg_cap ? n_raw : r.seg_cap;  // beyond: PF_STAGE was raised
+    if (lead) {
+      st_agent(&ctl->lvl[(l + 2) % 3], 0ull);
+      atomicAdd(&ctl->cand, (unsigned long long)n);
+    }
+    const uint64_t* src = r.stage[l & 1];
+    uint64_t* dst = r.stage[(l + 1) & 1];
+    for (uint64_t it = (uint64_t)blockIdx.x * PL * PAB; it < n; it += stride * PAB) {
+      uint64_t key[PAB];
+      bool nl[PAB];
+#pragma unroll
+      for (int u = 0; u < PAB; ++u) {
+        const uint64_t i = it + (uint64_t)u * PL + tid;
+        key[u] = i < n ? ld_agent(&src[i]) : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < PAB; ++u) {
+        const bool in = it + (uint64_t)u * PL + tid < n;
+        bool newo = false, news = false;
+        uint64_t okey = 0;
+        if (in) {
+          if (key[u] & DIRECT) {
+            okey = key[u] & ~DIRECT;
+            newo = set_insert(r.O, r.tmask, okey, r.ep, &ctl->flags);
+          } else {
+            news = set_insert(r.S, r.tmask, key[u], r.ep, &ctl->flags);
+            if (news && (key[u] & a.bitj)) {
+              okey = key[u] & ~a.bitj;
+              newo = set_insert(r.O, r.tmask, okey, r.ep, &ctl->flags);
+            }
+          }
+        }
+        expl += news;
+        nl[u] = news && !(key[u] & a.bitj);
+        listed += nl[u];
+        // OUT list append: one global atomic per wave
+        const unsigned long long m = __ballot(newo);
+        if (m) {
+          const int leader = __ffsll((long long)m) - 1;
+          unsigned long long base = 0;
+          if (lane == leader) base = atomicAdd(out_count, (unsigned long long)__popcll(m));
+          base = __shfl(base, leader, 64);
+          if (newo) {
+            const unsigned long long q = base + __popcll(m & ((1ull << lane) - 1));
+            if (q < r.list_cap) st_agent(&r.outl[q], okey);
+            else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+          }
+        }
+      }
+      emit<PAB>(a, key, nl, r.wd, mmask, dst, r.seg_cap, &ctl->lvl[(l + 1) % 3], ctl, s_w, &s_base);
+    }
+    if (!run_sync(r, &s_abort)) return;
+  }
+  // every level counter is zero again for the next step (lvl[(l + 2) % 3] held level l-1's)
+  if (lead) {
+    st_agent(&ctl->lvl[(l + 2) % 3], 0ull);
+    r.flog[r.flog_i] = ld_agent(out_count);
+    atomicAdd(&ctl->levels, (unsigned long long)(l + 1));
+    atomicAdd(&ctl->listed, (unsigned long long)nf);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    expl += __shfl_down(expl, off, 64);
+    listed += __shfl_down(listed, off, 64);
+  }
+  if (lane == 0 && expl) atomicAdd(&ctl->explored, expl);
+  if (lane == 0 && listed) atomicAdd(&ctl->listed, listed);
+}
+
 void set_msg(char* err, int32_t len, const char* fmt, ...) {
   if (!err || len <= 0) return;
   va_list ap;
@@ -303,6 +519,13 @@ struct lc_part {
   PartCtl* ctl = nullptr;
   PartCtl* hctl = nullptr;    // pinned host copy
   int grid = 1024;
+  // lc_part_run (world 1): second stage buffer, barrier words, per-step OUT counts
+  uint64_t* stage2 = nullptr;
+  PartBar* bar = nullptr;
+  unsigned long long* flog = nullptr;
+  unsigned long long* hflog = nullptr;
+  int run_grid = 0;
+  uint64_t run_cap = 0;       // entries of stage and stage2 as lc_part_run sized them
   // measurement: HIP events around each kernel (on the caller's stream), algorithmic bytes
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool absorb_pending = false;
@@ -320,9 +543,10 @@ struct lc_part {
 
   ~lc_part() {
     for (void* q : {(void*)S, (void*)O, (void*)F, (void*)OUTL, (void*)Lb[0], (void*)Lb[1], (void*)stage,
-                    (void*)ctl})
+                    (void*)ctl, (void*)stage2, (void*)bar, (void*)flog})
       if (q) (void)hipFree(q);
     if (hctl) (void)hipHostFree(hctl);
+    if (hflog) (void)hipHostFree(hflog);
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
   }
@@ -347,6 +571,30 @@ int part_read_ctl(lc_part* p, hipStream_t s, char* err, int32_t err_len) {
     if (hipEventElapsedTime(&ms, p->ev[2], p->ev[3]) == hipSuccess) p->kernel_ms += ms;
     p->absorb_pending = false;
   }
+  return 0;
+}
+
+// step t's invocations into the step arguments; a fresh set epoch (both sets cleared on wrap)
+int part_begin(lc_part* p, int64_t t, hipStream_t s, char* err, int32_t err_len) {
+  const Encoded& e = p->enc;
+  for (int64_t q = e.inv_off[t]; q < e.inv_off[t + 1]; ++q) {
+    const int k = e.inv_slot[q];
+    p->args.ops[k] = ((uint64_t)(uint32_t)(int32_t)e.inv_b[q] << 32) | (uint64_t)(uint32_t)(int32_t)e.inv_a[q];
+    p->live |= 1ull << k;
+  }
+  const int j = e.step_slot[t];
+  p->args.live = p->live;
+  p->args.bitj = 1ull << j;
+  p->args.mask_bits = p->mask_bits;
+  p->args.world = p->world;
+  p->args.rank = p->rank;
+  p->wd = (uint32_t)(64 - __builtin_clzll(p->live));
+  if (++p->epoch > EPOCH_MAX) {  // epochs wrapped: clear both sets once
+    PT_TRY(hipMemsetAsync(p->S, 0, sizeof(uint64_t) << p->slog, s));
+    PT_TRY(hipMemsetAsync(p->O, 0, sizeof(uint64_t) << p->slog, s));
+    p->epoch = 1;
+  }
+  p->t = t;
   return 0;
 }
 
@@ -449,27 +697,9 @@ int32_t lc_part_step_begin(lc_part* p, int64_t t, void* stream, char* err, int32
     set_msg(err, err_len, "step %lld out of order or history not searchable", (long long)t);
     return LC_E_ARG;
   }
-  hipStream_t s = (hipStream_t)stream;
   PT_TRY(hipSetDevice(p->device));
-  const Encoded& e = p->enc;
-  for (int64_t q = e.inv_off[t]; q < e.inv_off[t + 1]; ++q) {
-    const int k = e.inv_slot[q];
-    p->args.ops[k] = ((uint64_t)(uint32_t)(int32_t)e.inv_b[q] << 32) | (uint64_t)(uint32_t)(int32_t)e.inv_a[q];
-    p->live |= 1ull << k;
-  }
-  const int j = e.step_slot[t];
-  p->args.live = p->live;
-  p->args.bitj = 1ull << j;
-  p->args.mask_bits = p->mask_bits;
-  p->args.world = p->world;
-  p->args.rank = p->rank;
-  p->wd = (uint32_t)(64 - __builtin_clzll(p->live));
-  if (++p->epoch > EPOCH_MAX) {  // epochs wrapped: clear both sets once
-    PT_TRY(hipMemsetAsync(p->S, 0, sizeof(uint64_t) << p->slog, s));
-    PT_TRY(hipMemsetAsync(p->O, 0, sizeof(uint64_t) << p->slog, s));
-    p->epoch = 1;
-  }
-  p->t = t;
+  int rc = part_begin(p, t, (hipStream_t)stream, err, err_len);
+  if (rc) return rc;
   p->level = 0;
   p->cur = 0;
   return 0;
@@ -615,6 +845,134 @@ int32_t lc_part_results(lc_part* p, int64_t t, void* stream, int64_t* out4, char
   out4[2] = (t >= 0 && t < ns) ? p->enc.step_inv_idx[t] : -1;
   out4[3] = (t > 0 && t <= ns) ? p->enc.step_cmp_idx[t - 1] : -1;
   return 0;
+}
+
+/* World 1, device-resident: runs every RETURN step (or the first max_steps) with one
+ * cooperative launch per step that loops over the step's BFS levels behind grid barriers
+ * (part_step_kernel); the host reads the per-step frontier sizes once per 2,048 steps. Same
+ * verdict, failing step and explored count as the level protocol above. Call on a fresh plan.
+ * out4[0] steps run, [1] first failing step (-1: none), [2] BFS levels, [3] explored. */
+int32_t lc_part_run(lc_part* p, void* stream, int64_t max_steps, int64_t* out4, char* err, int32_t err_len) {
+  if (!p || !out4) return LC_E_ARG;
+  if (p->world != 1 || p->t != -1 || p->enc.err[0]) {
+    set_msg(err, err_len, "lc_part_run needs world 1, a fresh plan and a searchable history");
+    return LC_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  PT_TRY(hipSetDevice(p->device));
+  constexpr int64_t CHUNK = 2048;
+  if (!p->bar) {
+    PT_TRY(hipMalloc(&p->bar, sizeof(PartBar)));
+    PT_TRY(hipMemset(p->bar, 0, sizeof(PartBar)));
+    PT_TRY(hipMalloc(&p->flog, CHUNK * sizeof(unsigned long long)));
+    PT_TRY(hipHostMalloc(&p->hflog, CHUNK * sizeof(unsigned long long), hipHostMallocDefault));
+    int occ = 0;
+    PT_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, part_step_kernel, PL, 0));
+    hipDeviceProp_t prop;
+    PT_TRY(hipGetDeviceProperties(&prop, p->device));
+    if (occ < 1) {
+      set_msg(err, err_len, "part_step_kernel does not fit a CU");
+      return LC_E_DEVICE;
+    }
+    p->run_grid = prop.multiProcessorCount;  // one workgroup per CU: co-resident
+  }
+  const int64_t ns_all = p->enc.n_steps(0);
+  const int64_t ns = max_steps >= 0 ? std::min(ns_all, max_steps) : ns_all;
+  const uint64_t tb = sizeof(uint64_t) << p->slog;
+  for (int attempt = 0;; ++attempt) {
+    // two stage buffers of seg_cap >= list_cap candidates (a level's candidates)
+    const uint64_t want = std::max(p->seg_cap, p->list_cap);
+    if (!p->stage2 || want != p->run_cap) {
+      PT_TRY(hipFree(p->stage));
+      if (p->stage2) PT_TRY(hipFree(p->stage2));
+      p->stage = p->stage2 = nullptr;
+      PT_TRY(hipMalloc(&p->stage, sizeof(uint64_t) * want));
+      PT_TRY(hipMalloc(&p->stage2, sizeof(uint64_t) * want));
+      p->seg_cap = p->run_cap = want;
+    }
+    if (attempt) {  // start over: empty sets, the initial frontier {key 0}, zero counters
+      PT_TRY(hipMemsetAsync(p->S, 0, tb, s));
+      PT_TRY(hipMemsetAsync(p->O, 0, tb, s));
+      PT_TRY(hipMemsetAsync(p->ctl, 0, sizeof(PartCtl), s));
+      PT_TRY(hipMemsetAsync(p->F, 0, sizeof(uint64_t), s));
+      const unsigned long long one = 1;
+      PT_TRY(hipMemcpyAsync(&p->ctl->oc[1], &one, sizeof one, hipMemcpyHostToDevice, s));
+      PT_TRY(hipStreamSynchronize(s));
+      p->epoch = 0;
+      p->live = 0;
+      p->args = StepArgs{};
+      p->t = -1;
+      p->sp = 0;
+    }
+    PT_TRY(hipEventRecord(p->ev[0], s));
+    int64_t t = 0, fail = -1;
+    uint64_t flags = 0;
+    while (t < ns && fail < 0) {
+      const int64_t c0 = t, c1 = std::min(ns, t + CHUNK);
+      for (; t < c1; ++t) {
+        int rc = part_begin(p, t, s, err, err_len);
+        if (rc) return rc;
+        RunArgs r{};
+        r.S = p->S;
+        r.O = p->O;
+        r.tmask = (1ull << p->slog) - 1;
+        r.F = p->F;
+        r.outl = p->OUTL;
+        r.list_cap = p->list_cap;
+        r.stage[0] = p->stage;
+        r.stage[1] = p->stage2;
+        r.seg_cap = p->seg_cap;
+        r.ctl = p->ctl;
+        r.bar = p->bar;
+        r.flog = p->flog;
+        r.flog_i = (uint32_t)(t - c0);
+        r.sp = p->sp;
+        r.ep = p->epoch;
+        r.wd = p->wd;
+        r.nwg = (uint32_t)p->run_grid;
+        void* kargs[] = {(void*)&p->args, (void*)&r};
+        PT_TRY(hipLaunchCooperativeKernel((const void*)part_step_kernel, dim3(p->run_grid), dim3(PL), kargs, 0, s));
+        std::swap(p->F, p->OUTL);  // OUT becomes the frontier
+        p->live &= ~p->args.bitj;
+        p->sp ^= 1;
+      }
+      PT_TRY(hipMemcpyAsync(p->hflog, p->flog, sizeof(unsigned long long) * (size_t)(c1 - c0),
+                            hipMemcpyDeviceToHost, s));
+      int rc = part_read_ctl(p, s, err, err_len);
+      if (rc) return rc;
+      flags = p->hctl->flags;
+      if (flags) break;
+      for (int64_t i = 0; i < c1 - c0; ++i)
+        if (p->hflog[i] == 0) {
+          fail = c0 + i;
+          break;
+        }
+    }
+    PT_TRY(hipEventRecord(p->ev[1], s));
+    int rc = part_read_ctl(p, s, err, err_len);
+    if (rc) return rc;
+    flags = p->hctl->flags;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p->ev[0], p->ev[1]) == hipSuccess) p->kernel_ms += ms;
+    if (flags & PF_ABORT) {
+      set_msg(err, err_len, "part_step_kernel: grid barrier watchdog expired");
+      return LC_E_DEVICE;
+    }
+    if ((flags & PF_STAGE) && attempt < 3) {
+      p->seg_cap *= 4;  // a level outgrew the stage: start over with 4x
+      continue;
+    }
+    if (flags & (PF_OVERFLOW | PF_STAGE)) {
+      set_msg(err, err_len, "frontier exceeded the partition capacity (LC_H_CAPACITY)");
+      return LC_H_CAPACITY;
+    }
+    p->alg_bytes += 8.0 * (double)p->hctl->listed + 24.0 * (double)p->hctl->cand;
+    out4[0] = fail >= 0 ? fail + 1 : t;
+    out4[1] = fail;
+    out4[2] = (int64_t)p->hctl->levels;
+    out4[3] = (int64_t)p->hctl->explored;
+    return 0;
+  }
 }
 
 void lc_part_destroy(lc_part* p) { delete p; }

@@ -18,7 +18,7 @@ EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_shard_histories"
            "lc_plan_stats", "lc_plan_destroy", "lc_bounds_plan_create", "lc_bounds_plan_sums",
            "lc_bounds_plan_run", "lc_bounds_plan_destroy", "lc_part_create", "lc_part_info",
            "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
-           "lc_part_step_end", "lc_part_results", "lc_part_destroy")
+           "lc_part_step_end", "lc_part_results", "lc_part_run", "lc_part_destroy")
 STATS_N = 31
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
@@ -94,6 +94,8 @@ def load():
     L.lc_part_step_end.restype = C.c_int32
     L.lc_part_results.argtypes = [P, C.c_int64, P, P, C.c_char_p, C.c_int32]
     L.lc_part_results.restype = C.c_int32
+    L.lc_part_run.argtypes = [P, P, C.c_int64, P, C.c_char_p, C.c_int32]
+    L.lc_part_run.restype = C.c_int32
     L.lc_part_destroy.argtypes = [P]
     L.lc_part_destroy.restype = None
     if L.lc_abi_version() != 1:
@@ -332,6 +334,13 @@ class PartPlan:
         out = np.zeros(1, np.int64)
         self._call(self._L.lc_part_step_end, stream, _p(out))
         return int(out[0])
+
+    def run(self, stream=None, max_steps: int = -1):
+        """World 1, device-resident level loop (lc_part_run) on a fresh plan ->
+        (steps run, first failing step or -1, BFS levels, explored)."""
+        out = np.zeros(4, np.int64)
+        self._call(self._L.lc_part_run, stream, max_steps, _p(out))
+        return tuple(int(x) for x in out)
 
     def results(self, t: int, stream=None):
         """-> (this rank's explored, fail :index, its invocation's :index, previous :ok's)"""

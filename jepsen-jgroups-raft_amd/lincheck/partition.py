@@ -74,11 +74,15 @@ class _Exchange:
         return int(t[0].item()), bool(t[1].item())
 
 
-def search(plan, tdist=None, device="cpu", stream=None, max_steps=None):
+def search(plan, tdist=None, device="cpu", stream=None, max_steps=None, device_loop=True):
     """Run the partitioned search of `plan` (this rank's part) to the end. Returns
     {"valid": 1/0/2, "fail_step", "fail_idx", "fail_inv", "prev_ok", "explored", "err",
-     "steps", "levels", "exchanged_bytes", "wall_s"} — identical on every rank."""
+     "steps", "levels", "exchanged_bytes", "wall_s"} — identical on every rank. At world 1 a
+    plan with `run` (the HIP plan) keeps the whole level loop on the device (lc_part_run)
+    unless device_loop is False."""
     ex = _Exchange(tdist, device)
+    if ex.world == 1 and device_loop and hasattr(plan, "run") and not plan.err:
+        return _search_device(plan, stream, max_steps)
     world, rank = ex.world, ex.rank
     state = {"send": None, "recv": None}
 
@@ -165,8 +169,28 @@ def search(plan, tdist=None, device="cpu", stream=None, max_steps=None):
             "wall_s": time.perf_counter() - t0}
 
 
+def _search_device(plan, stream, max_steps):
+    t0 = time.perf_counter()
+    try:
+        steps, fail_t, levels, explored = plan.run(stream, -1 if max_steps is None else max_steps)
+        valid, err = (0 if fail_t >= 0 else 1), 0
+    except _lib.CapacityError:
+        steps, fail_t, levels, explored = 0, -1, 0, 0
+        valid, err = 2, _lib.PartPlan.H_CAPACITY
+    res = plan.results(fail_t if fail_t >= 0 else steps - 1, stream)
+    if valid == 2:
+        explored = res[0]
+    st = plan.stats()
+    return {"valid": valid, "fail_step": fail_t,
+            "fail_idx": res[1] if valid == 0 else -1, "fail_inv": res[2] if valid == 0 else -1,
+            "prev_ok": res[3] if valid == 0 else -1, "explored": explored, "err": err,
+            "steps": steps, "levels": levels, "exchanged_bytes": 0,
+            "kernel_ms": st["kernel_ms"], "alg_bytes": st["alg_bytes"],
+            "wall_s": time.perf_counter() - t0}
+
+
 def check_partitioned(h, hist: int = 0, tdist=None, device_index: int | None = None,
-                      capacity_log2: int = 0):
+                      capacity_log2: int = 0, device_loop: bool = True):
     """Check history `hist` of h with its frontier partitioned over the ranks of `tdist`
     (torch.distributed, initialised; None = one rank) on this rank's GPU."""
     world = tdist.get_world_size() if tdist is not None else 1
@@ -183,6 +207,6 @@ def check_partitioned(h, hist: int = 0, tdist=None, device_index: int | None = N
     plan = _lib.PartPlan(h, hist=hist, rank=rank, world=world, device=device_index,
                          capacity_log2=capacity_log2)
     try:
-        return search(plan, tdist, device, stream)
+        return search(plan, tdist, device, stream, device_loop=device_loop)
     finally:
         plan.close()

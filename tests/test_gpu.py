@@ -695,10 +695,11 @@ def _part_cases():
     return hs
 
 
-def test_gpu_partitioned_world1_vs_oracle():
+@pytest.mark.parametrize("device_loop", [True, False], ids=["lc_part_run", "level_protocol"])
+def test_gpu_partitioned_world1_vs_oracle(device_loop):
     from lincheck import partition
     for i, h in enumerate(_part_cases()):
-        r = partition.check_partitioned(h)
+        r = partition.check_partitioned(h, device_loop=device_loop)
         assert _part_row(r) == _oracle_part_row(h), (i, r)
 
 
@@ -706,15 +707,41 @@ def test_gpu_partitioned_matches_dense_on_c2_slice():
     from lincheck import partition
     h = synth.gen_config("c2", scale=0.3)
     r = partition.check_partitioned(h)
+    q = partition.check_partitioned(h, device_loop=False)
     g = _lib.check(1, 0, h)
     assert (r["valid"], r["explored"]) == (int(g["valid"][0]), int(g["explored"][0]))
+    assert (q["valid"], q["explored"], q["levels"]) == (r["valid"], r["explored"], r["levels"])
 
 
-def test_gpu_partitioned_capacity_is_unknown():
+@pytest.mark.parametrize("device_loop", [True, False], ids=["lc_part_run", "level_protocol"])
+def test_gpu_partitioned_capacity_is_unknown(device_loop):
     from lincheck import partition
     h = synth.gen_config("c2", scale=0.1)
-    r = partition.check_partitioned(h, capacity_log2=10)
+    r = partition.check_partitioned(h, capacity_log2=10, device_loop=device_loop)
     assert r["valid"] == 2 and r["err"] == -7
+
+
+def test_gpu_partitioned_run_stage_retry_and_max_steps():
+    """lc_part_run with lists of 2^11: levels whose candidates outgrow the stage make it start
+    over with a 4x stage (same answer as the oracle when the sets still fit); max_steps stops
+    early with the explored count of the steps run."""
+    from lincheck import partition
+    for h in _part_cases()[:4]:
+        r = partition.check_partitioned(h, capacity_log2=11)
+        if r["err"] == 0:
+            assert _part_row(r) == _oracle_part_row(h)
+    h = _part_cases()[0]
+    plan = _lib.PartPlan(h)
+    try:
+        steps, fail, levels, explored = plan.run(None, 40)
+    finally:
+        plan.close()
+    q = _lib.PartPlan(h)
+    try:
+        full = partition.search(q, max_steps=40, device_loop=False)
+    finally:
+        q.close()
+    assert (steps, fail, levels, explored) == (40, -1, full["levels"], full["explored"])
 
 
 def _gpu_part_worker(rank, world, port, q):
