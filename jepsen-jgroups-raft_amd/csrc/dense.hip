@@ -354,6 +354,25 @@ __device__ __forceinline__ int team_any(int v) {
   else return __any(v);
 }
 
+// Barrier of the TEAM/64 waves of a sub-workgroup team: one lane per wave arrives on an LDS
+// counter (qb[0]), the last arriver bumps the generation (qb[1]) the others poll.
+template <int TEAM>
+__device__ __forceinline__ void sub_sync(unsigned* qb) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned g = __hip_atomic_load(&qb[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__hip_atomic_fetch_add(&qb[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == TEAM / 64 - 1) {
+      __hip_atomic_store(&qb[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&qb[1], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      while (__hip_atomic_load(&qb[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == g)
+        __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // binomials and the first entry of each popcount layer of the `lbits`-bit word list
 __device__ __forceinline__ void init_tables(uint32_t* binom, uint32_t* wofs, int lbits, int nthreads) {
   const int tid = threadIdx.x;
@@ -566,11 +585,18 @@ __device__ __forceinline__ T rdl(T v, int l) {
 // starts after a barrier with ONE lane-parallel read of the ring: lane i holds the header of
 // step t_ret + i. Retirement (in order, with the failure test), the running steps' layers
 // ("segments") and the next start all come from that view by ballots and readlanes.
-template <int TEAM, int TLOG, int RING>
+// SUB: the team is TEAM/64 waves of a larger workgroup (big_mid_mode), synchronised through
+// its own LDS barrier words qb (s_barrier would stop every wave of the workgroup).
+template <int TEAM, int TLOG, int RING, bool SUB = false>
 __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, const uint64_t* zero,
                                              PipeStep* ring, int* sQ, unsigned long long* sExpl,
                                              const uint32_t* words_g, const uint32_t* wofs_g, const uint32_t* binom,
-                                             int tt, unsigned long long& st_fout, unsigned long long& st_steps) {
+                                             int tt, unsigned long long& st_fout, unsigned long long& st_steps,
+                                             unsigned* qb = nullptr) {
+  auto tsync = [&]() {
+    if constexpr (SUB) sub_sync<TEAM>(qb);
+    else team_sync<TEAM>();
+  };
   // pull batches read entries up to OP_PAD + b0 + 6 (b0 < H, a multiple of 4); slots < TLOG
   static_assert(OP_PAD + ((TLOG - 4) / 4) * 4 + 6 < PIPE_OPN && OP_PAD + TLOG <= PIPE_OPN, "op table too small");
   static_assert(RING <= 64, "one lane per ring entry");
@@ -580,10 +606,10 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
   const bool decoder = tt >= TEAM - 64;
   for (;;) {
     if (tt == 0) *sQ = atomicAdd(p.queue, 1);
-    team_sync<TEAM>();
+    tsync();
     const int qi = *sQ;
     if (tt == 0) *sExpl = 0;
-    team_sync<TEAM>();
+    tsync();
     if (qi >= p.n) break;
     const int h = p.order[qi];
     if (p.stamps && tt == 0) p.stamps[4 * h] = __builtin_amdgcn_s_memrealtime();
@@ -606,7 +632,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
           for (int q = 0; q < tt; ++q) o += binom[Hh * BINOM_N + q];
           lo[tt] = o;
         }
-        team_sync<TEAM>();
+        tsync();
         for (int q = 0; q <= Hh; ++q) {
           const uint32_t nq = binom[Hh * BINOM_N + q], og = wofs_g[q], ol = lo[q];
           for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)TEAM) lw[ol + r] = words_g[og + r];
@@ -614,7 +640,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
         words = lw, wofs = lo;
       }
     }
-    team_sync<TEAM>();
+    tsync();
     if (tt == 0) B[0] = 1;  // (cas-register) starts at nil: state id 0, nothing linearized
     StreamWin sw;
     int64_t pos = p.sbeg[h];
@@ -622,7 +648,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       pipe_decode(p, sw, pos, lane, &ring[0], nullptr);
       if (lane == 0) ring[0].start = 0;  // (the decoder wave, after its own stores)
     }
-    team_sync<TEAM>();
+    tsync();
     unsigned long long expl = 0;
     int fail_t = -1;
     int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0;  // decoded, started, retired
@@ -799,7 +825,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
         }
       }
       mark(2);
-      team_sync<TEAM>();
+      tsync();
       mark(3);
     }
     if (prof) {
@@ -820,13 +846,22 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
         st_fout += (uint32_t)__popcll(X);
         nzx |= X;
       }
-      if (!team_any<TEAM>(nzx != 0)) fail_t = ns - 1;
+      if constexpr (SUB) {
+        const bool anyw = __any(nzx != 0);  // (every lane votes)
+        if ((tt & 63) == 0 && anyw) atomicOr(&qb[2], 1u);
+        tsync();
+        if (!qb[2]) fail_t = ns - 1;
+        tsync();
+        if (tt == 0) qb[2] = 0;
+      } else if (!team_any<TEAM>(nzx != 0)) {
+        fail_t = ns - 1;
+      }
     }
     if (tt == 0) st_steps += fail_t >= 0 ? fail_t + 1 : ns;
     for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
     if constexpr (TEAM >= 256) {
       if (lane == 0 && expl) atomicAdd(sExpl, expl);
-      __syncthreads();
+      tsync();
       expl = *sExpl;
     } else {
       expl = __shfl(expl, 0, 64);
@@ -837,16 +872,20 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
       if (p.stamps) p.stamps[4 * h + 1] = __builtin_amdgcn_s_memrealtime();
     }
-    team_sync<TEAM>();
+    tsync();
   }
 }
 
 // launch statistics (per wave, one atomic each)
+// (st_steps is held by each team's first thread, zero elsewhere: summed over every wave)
 __device__ __forceinline__ void flush_stats(const DenseParams& p, unsigned long long st_fout,
-                                            unsigned long long st_steps, bool step_owner) {
-  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
+                                            unsigned long long st_steps, bool /*step_owner*/) {
+  for (int off = 32; off > 0; off >>= 1) {
+    st_fout += __shfl_down(st_fout, off, 64);
+    st_steps += __shfl_down(st_steps, off, 64);
+  }
   if ((threadIdx.x & 63) == 0 && st_fout) atomicAdd(&p.stats[SS_FOUT], st_fout);
-  if (step_owner && st_steps) atomicAdd(&p.stats[SS_STEPS], st_steps);
+  if ((threadIdx.x & 63) == 0 && st_steps) atomicAdd(&p.stats[SS_STEPS], st_steps);
 }
 
 constexpr int WAVE_WG = 256;
@@ -1382,6 +1421,50 @@ __device__ __forceinline__ void big_wave_mode(const DenseParams& p, uint64_t* sT
   __syncthreads();
 }
 
+// MID histories (widths 12..DENSE_MID_LMAX) inside a big workgroup (LC_PIPE bit 7): its 16
+// waves are 4 MID teams of 4 waves (history_pipe<256, SUB>), each on a 16 KiB quarter of the
+// LDS table with a ring of its own and its own LDS barrier, dequeuing from the MID queue. A
+// BLOCK team's narrow steps keep only a few of its 16 waves busy (a width-12 super-layer is
+// ~256 words), so four histories share the CU instead of one.
+constexpr int QUAD_RING = 8;
+__device__ __forceinline__ void big_mid_mode(const DenseParams& p, uint64_t* sTab, const uint64_t* zero,
+                                             const uint32_t* binom, int tid, unsigned long long& st_fout,
+                                             unsigned long long& st_steps) {
+  constexpr int NQ = 4, HQ = DENSE_MID_LMAX - 3, TABQ = 1 << HQ;
+  uint64_t* const tabs = sTab;                                             // NQ tables of TABQ words
+  PipeStep* const rings = reinterpret_cast<PipeStep*>(sTab + NQ * TABQ);  // NQ rings
+  unsigned long long* const sEx = reinterpret_cast<unsigned long long*>(rings + NQ * QUAD_RING);
+  uint32_t* const words = reinterpret_cast<uint32_t*>(sEx + NQ);          // HQ-bit word list
+  uint32_t* const wofs = words + TABQ;                                     // its layer offsets
+  int* const sQq = reinterpret_cast<int*>(wofs + 16);
+  unsigned* const qbar = reinterpret_cast<unsigned*>(sQq + NQ);           // per team: count, gen, any
+  static_assert((NQ * TABQ) * 8 + NQ * QUAD_RING * sizeof(PipeStep) + NQ * 8 + TABQ * 4 + 16 * 4 + NQ * 4 +
+                        NQ * 4 * 4 <= (1 << (DENSE_LMAX - 3)) * 8,
+                "MID mode fits the big table");
+  __syncthreads();  // the table's previous users are done
+  if (tid <= HQ + 1) {
+    uint32_t o = 0;
+    for (int q = 0; q < tid; ++q) o += binom[HQ * BINOM_N + q];
+    wofs[tid] = o;
+  }
+  if (tid < NQ * 4) qbar[tid] = 0;
+  __syncthreads();
+  for (int v = tid; v < TABQ; v += 1024) {  // colex rank within its popcount layer
+    uint32_t rank = 0;
+    int i = 0;
+    for (uint32_t x = (uint32_t)v; x; x &= x - 1, ++i) rank += binom[__builtin_ctz(x) * BINOM_N + i + 1];
+    words[wofs[__popc(v)] + rank] = (uint32_t)v;
+  }
+  __syncthreads();
+  DenseParams q = p;
+  q.n = p.n2, q.order = p.order2, q.queue = p.queue2;
+  const int team = tid / 256;
+  history_pipe<256, DENSE_MID_LMAX, QUAD_RING, true>(q, tabs + team * TABQ, zero, rings + team * QUAD_RING,
+                                                     &sQq[team], &sEx[team], words, wofs, binom, tid & 255,
+                                                     st_fout, st_steps, qbar + team * 4);
+  __syncthreads();
+}
+
 // BLOCK histories and TILE teams in one launch (same 1024-thread, 128 KiB-LDS workgroups, so
 // every workgroup is resident: the grid never exceeds one workgroup per CU).
 //
@@ -1426,15 +1509,23 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   if ((int)blockIdx.x >= p.n_team_wgs) {  // ------------------------------- BLOCK histories
     // the last ceil(n_w / 16) workgroups start on the WAVE queue: a WAVE history is a long
     // latency-bound chain, and started after the BLOCK queue it would be the launch's tail
-    if (p.n_w > 0 && (int)blockIdx.x >= (int)gridDim.x - (p.n_w + 15) / 16)
+    const int wave_first = p.n_w > 0 ? (p.n_w + 15) / 16 : 0;
+    if (wave_first && (int)blockIdx.x >= (int)gridDim.x - wave_first)
       big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
+    // and the next mid_first start on the MID queue (long chains too, four per workgroup)
+    else if (p.n2 > 0 && (p.pipe & 128) && (int)blockIdx.x >= (int)gridDim.x - wave_first - p.mid_first)
+      big_mid_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     if (p.pipe & 1) {
       history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
                                                  st_fout, st_steps);
-      DenseParams q2 = p;  // then help with the MID queue
-      q2.n = p.n2, q2.order = p.order2, q2.queue = p.queue2;
-      history_pipe<1024, DENSE_LMAX, BLOCK_RING>(q2, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
-                                                 st_fout, st_steps);
+      if (p.n2 > 0 && (p.pipe & 128)) {  // then the MID queue, four histories per workgroup
+        big_mid_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
+      } else {
+        DenseParams q2 = p;  // then help with the MID queue
+        q2.n = p.n2, q2.order = p.order2, q2.queue = p.queue2;
+        history_pipe<1024, DENSE_LMAX, BLOCK_RING>(q2, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom,
+                                                   tid, st_fout, st_steps);
+      }
     } else
       history_loop<1024, DENSE_LMAX>(p, sTab, &sZero, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout,
                                      st_steps);
@@ -1487,6 +1578,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     __syncthreads();
     history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
                                                st_fout, st_steps);
+    if (p.n2 > 0 && (p.pipe & 128)) big_mid_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     if (p.n_w > 0) big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     flush_stats(p, st_fout, st_steps, tid == 0);
     return;
@@ -1785,10 +1877,14 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     __syncthreads();
     history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
                                                st_fout, st_steps);
-    DenseParams q2 = p;
-    q2.n = p.n2, q2.order = p.order2, q2.queue = p.queue2;
-    history_pipe<1024, DENSE_LMAX, BLOCK_RING>(q2, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
-                                               st_fout, st_steps);
+    if (p.n2 > 0 && (p.pipe & 128)) {
+      big_mid_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
+    } else {
+      DenseParams q2 = p;
+      q2.n = p.n2, q2.order = p.order2, q2.queue = p.queue2;
+      history_pipe<1024, DENSE_LMAX, BLOCK_RING>(q2, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom,
+                                                 tid, st_fout, st_steps);
+    }
     if (p.n_w > 0) big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
   }
   flush_stats(p, st_fout, st_steps, tid == 0);

@@ -142,8 +142,9 @@ struct lc_plan {
   // teams without per-step team barriers (finished teams then join the BLOCK queue); bit 4 =
   // MID teams for widths 12..14 (needs bit 0); bit 5 = one pass per running segment (r1 form;
   // default: segments packed over the team); bit 6 = WAVE histories on the big kernel's waves
-  // (no dense_wave_kernel). Default 79 = 1|2|4|8|64, with the team planner (plan_teams).
-  int dense_pipe = 79;
+  // (no dense_wave_kernel); bit 7 = MID histories (widths 12..mid_maxw) as 4-wave teams inside
+  // big workgroups (no dense_mid_kernel). Default 207 = 1|2|4|8|64|128, with the team planner.
+  int dense_pipe = 207;
   std::vector<int> plan_lb;  // team planner: local slots per tile (0: not a team)
   bool plan_off = false;     // LC_TEAM_PLAN=0: every wide history keeps 17-bit tiles
   hipStream_t stream2 = nullptr, stream3 = nullptr;
@@ -266,6 +267,7 @@ struct lc_plan {
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e);
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
     if ((e = getenv("LC_PLAN_K")) && atof(e) > 0) plan_k16 = atof(e);
+    if ((e = getenv("LC_MID_MAXW")) && atoi(e) > DENSE_WAVE_LMAX && atoi(e) <= DENSE_MID_LMAX) mid_maxw = atoi(e);
     if ((e = getenv("LC_TILE_WIDE")) && strchr(e, ':')) {
       wide_from = atoi(e);
       wide_lbits = std::max(12, std::min(atoi(strchr(e, ':') + 1), DENSE_LMAX));
@@ -413,10 +415,15 @@ struct lc_plan {
       if (!ok[h]) continue;
       const int lw = enc.live_max[h];
       // MID teams (several per CU) take the narrower BLOCK histories when BLOCK steps are pipelined
-      (lw <= DENSE_WAVE_LMAX ? dense_w : (lw <= DENSE_MID_LMAX && (dense_pipe & 17) == 17) ? dense_m
+      (lw <= DENSE_WAVE_LMAX ? dense_w
+       : ((dense_pipe & 129) == 129 ? lw <= mid_maxw : lw <= DENSE_MID_LMAX && (dense_pipe & 17) == 17) ? dense_m
        : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
     }
     plan_teams(widths);
+    pool_block_us = 0, pool_mid_us = 0, pool_wave_us = 0;  // the BLOCK pool's planned work
+    for (int h : dense_b) pool_block_us += est_block_us(widths[h]);
+    if (dense_pipe & 128) for (int h : dense_m) pool_mid_us += est_mid_us(widths[h]) / 4.0;
+    if (dense_pipe & 64) for (int h : dense_w) pool_wave_us += 7.9 * (double)widths[h].size() / 16.0;
     auto heavy_first = [&](int a, int b) { return cost[a] > cost[b]; };
     std::stable_sort(dense_b.begin(), dense_b.end(), heavy_first);
     std::stable_sort(dense_w.begin(), dense_w.end(), heavy_first);
@@ -461,7 +468,16 @@ struct lc_plan {
     for (uint8_t L : ws) t += 4.67 + 0.00266 * std::ldexp(1.0, std::max(0, (int)L - 3));
     return t;
   }
-  double plan_k16 = 1.3;  // LC_PLAN_K: scales the team model's VALU term (r2p sweep: 1.3 best on C3)
+  // MID step (4-wave team, LC_PIPE bit 7)   4.9 + 0.0016 * 2^(L-3)  (r2t LC_DEBUG, C3)
+  static double est_mid_us(const std::vector<uint8_t>& ws) {
+    double t = 0;
+    for (uint8_t L : ws) t += 4.9 + 0.0016 * std::ldexp(1.0, std::max(0, (int)L - 3));
+    return t;
+  }
+  double pool_block_us = 0, pool_mid_us = 0, pool_wave_us = 0;  // the planned pool's work (WG-us)
+  int mid_maxw = 14;       // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7)
+  double plan_k16 = 0.7;  // LC_PLAN_K: scales the team model's VALU term (r2x sweep with MID
+                          // histories in big workgroups: 0.6-0.7 best on C3)
   double est_team_us(const std::vector<uint8_t>& ws, int lb) const {
     double t = 0;
     for (uint8_t L : ws) {
@@ -485,6 +501,8 @@ struct lc_plan {
     for (int h : dense_b) in_block[h] = 1, est[h] = est_block_us(ws[h]), pool += est[h];
     if (dense_pipe & 64)  // WAVE histories on the big kernel's waves, 16 per workgroup
       for (int h : dense_w) pool += 7.9 * (double)ws[h].size() / 16.0;
+    if (dense_pipe & 128)  // MID histories on the big kernel's waves, 4 per workgroup
+      for (int h : dense_m) pool += est_mid_us(ws[h]) / 4.0;
     std::vector<int> cand(dense_x);
     for (int h : dense_b)
       if (enc.live_max[h] >= 14) cand.push_back(h);
@@ -658,7 +676,9 @@ struct lc_plan {
       HIP_TRY(hipEventRecord(ev_w1, stream2));
       HIP_TRY(hipEventRecord(ev_join, stream2));
     }
-    if (nm) {
+    // LC_PIPE bit 7: MID histories run on the big kernel's waves, four per workgroup
+    const bool mid_in_big = (dense_pipe & 128) != 0;
+    if (nm && !mid_in_big) {
       if (!nw || wave_in_big) HIP_TRY(hipEventRecord(ev_fork, stream));
       HIP_TRY(hipStreamWaitEvent(stream3, ev_fork, 0));
       DenseParams q = p;
@@ -722,11 +742,19 @@ struct lc_plan {
         }
       }
       const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n + q.n2 + (q.n_w + 15) / 16));
+      // BLOCK-pool workgroups that start on the MID queue: its share of the pool's work
+      q.mid_first = 0;
+      if (mid_in_big && q.n2 > 0) {
+        const int pool_wgs = grid - twgs - (q.n_w + 15) / 16;
+        const double tot = pool_block_us + pool_mid_us + pool_wave_us;
+        const double share = tot > 0 ? pool_mid_us / tot : 0.0;
+        q.mid_first = std::max(0, std::min({(q.n2 + 3) / 4, pool_wgs, (int)std::lround(share * (grid - twgs))}));
+      }
       if (grid > 0) HIP_TRY(launch_dense(q, DENSE_BIG, grid, stream));
     }
     HIP_TRY(hipEventRecord(ev_b1, stream));
     if (nw && !wave_in_big) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
-    if (nm) HIP_TRY(hipStreamWaitEvent(stream, ev_join3, 0));
+    if (nm && !mid_in_big) HIP_TRY(hipStreamWaitEvent(stream, ev_join3, 0));
     HIP_TRY(hipEventRecord(ev1, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     float t = 0;
@@ -750,7 +778,7 @@ struct lc_plan {
     for (int i = 0; i < SS_N; ++i) ss[i] = ss3[i] + ss3[SS_N + i] + ss3[2 * SS_N + i];
     for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
       for (int h : *ids) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
-    stats[1] += (nw && !wave_in_big ? 1 : 0) + (nm ? 1 : 0) + (double)launches.size();
+    stats[1] += (nw && !wave_in_big ? 1 : 0) + (nm && !mid_in_big ? 1 : 0) + (double)launches.size();
     stats[12] += nb + nw + nx + nm;
     stats[13] += t;
     // per-kernel time (events on each kernel's own stream) and algorithmic bytes of the steps
@@ -759,13 +787,13 @@ struct lc_plan {
     HIP_TRY(hipEventElapsedTime(&tb, ev_b0, ev_b1));
     if (nw && !wave_in_big) HIP_TRY(hipEventElapsedTime(&tw, ev_w0, ev_w1));
     float tm = 0;  // the MID kernel runs beside both; its steps are counted with the wave kernel's
-    if (nm) HIP_TRY(hipEventElapsedTime(&tm, ev_m0, ev_m1));
+    if (nm && !mid_in_big) HIP_TRY(hipEventElapsedTime(&tm, ev_m0, ev_m1));
     stats[14] += tb;
     stats[15] += std::max(tw, tm);
     for (const std::vector<int>* ids : {&dense_b, &dense_x, &dense_w, &dense_m})
       for (int h : *ids) {
         const StepBytes b = dense_hist_bytes(h, fs[h]);
-        const int k = ((ids == &dense_w && !wave_in_big) || ids == &dense_m) ? 18 : 16;
+        const int k = ((ids == &dense_w && !wave_in_big) || (ids == &dense_m && !mid_in_big)) ? 18 : 16;
         stats[k] += b.hbm;
         stats[k + 1] += b.lds;
       }
@@ -778,12 +806,13 @@ struct lc_plan {
       double ex_big = 0, ex_wave = 0;
       for (const std::vector<int>* ids : {&dense_b, &dense_x}) for (int h : *ids) ex_big += (double)ex[h];
       for (const std::vector<int>* ids : {&dense_w, &dense_m})
-        for (int h : *ids) (ids == &dense_w && wave_in_big ? ex_big : ex_wave) += (double)ex[h];
+        for (int h : *ids)
+          ((ids == &dense_w ? wave_in_big : mid_in_big) ? ex_big : ex_wave) += (double)ex[h];
       const double fo_big = (double)ss3[SS_FOUT], fo_wave = (double)(ss3[SS_N + SS_FOUT] + ss3[2 * SS_N + SS_FOUT]);
-      stats[25] += fo_big + (nb + nx + (wave_in_big ? nw : 0));
+      stats[25] += fo_big + (nb + nx + (wave_in_big ? nw : 0) + (mid_in_big ? nm : 0));
       stats[26] += fo_big;
       stats[27] += ex_big;
-      stats[28] += fo_wave + ((wave_in_big ? 0 : nw) + nm);
+      stats[28] += fo_wave + ((wave_in_big ? 0 : nw) + (mid_in_big ? 0 : nm));
       stats[29] += fo_wave;
       stats[30] += ex_wave;
     }
