@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -875,6 +876,8 @@ int32_t lc_part_run(lc_part* p, void* stream, int64_t max_steps, int64_t* out4, 
       return LC_E_DEVICE;
     }
     p->run_grid = prop.multiProcessorCount;  // one workgroup per CU: co-resident
+    if (const char* e = getenv("LC_PART_GRID"))  // (tuning) fewer workgroups: cheaper barriers
+      if (atoi(e) >= 1 && atoi(e) < p->run_grid) p->run_grid = atoi(e);
   }
   const int64_t ns_all = p->enc.n_steps(0);
   const int64_t ns = max_steps >= 0 ? std::min(ns_all, max_steps) : ns_all;

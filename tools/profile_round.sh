@@ -32,9 +32,6 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
   --output-format csv -d $out/c2_pmc_sq -o run -- python -u bench.py --workload c2 --no-cpu --e2e-reps 0 --steps 1 \
   --warmup 0 >> $out/pmc.log 2>&1 || exit 1
-# partitioned frontier (axis 2, world 1) on a C2 slice: kernel trace, then the atomic counters
-PP="python -u bench.py --workload c2 --partition --scale 0.3 --steps 1 --warmup 0"
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $out/part_trace -o run -- $PP > $out/part_trace.log 2>&1 || exit 1
-timeout -s KILL 300 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TCP_TCC_ATOMIC_WITH_RET_REQ_sum \
-  TCP_TCC_ATOMIC_WITHOUT_RET_REQ_sum --output-format csv -d $out/part_pmc_atomic -o run -- $PP > $out/part_pmc.log 2>&1 || exit 1
+# partitioned frontier: tools/profile_part.sh (its own call: rocprofv3 segfaults at exit after
+# tracing the cooperative part_step_kernel, once the trace is written)
 echo done

@@ -1,0 +1,4 @@
+set -o pipefail
+o=gpurun_out/r2z; mkdir -p $o
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $o/pytest.log 2>&1 || exit 1
+echo done
