@@ -1440,6 +1440,7 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx, in
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n) {
   if (!p || !stats) return LC_E_ARG;
   for (int i = 0; i < n && i < LC_STATS_N; ++i) stats[i] = p->stats[i];
+  for (int i = 20; i < 25 && i < n; ++i) stats[i] = p->phase_ms[i - 20];  // creation phases, run or not
   return 0;
 }
 
