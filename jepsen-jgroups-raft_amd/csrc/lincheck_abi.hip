@@ -267,6 +267,8 @@ struct lc_plan {
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e);
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
     if ((e = getenv("LC_PLAN_K")) && atof(e) > 0) plan_k16 = atof(e);
+    if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
+    if ((e = getenv("LC_TEAM_ROT_LB"))) rot_min_lb = atoi(e);
     if ((e = getenv("LC_MID_MAXW")) && atoi(e) > DENSE_WAVE_LMAX && atoi(e) <= DENSE_MID_LMAX) mid_maxw = atoi(e);
     if ((e = getenv("LC_TILE_WIDE")) && strchr(e, ':')) {
       wide_from = atoi(e);
@@ -345,6 +347,17 @@ struct lc_plan {
     return b;
   }
 
+  // local slots per tile of wide history h: the team planner's choice, else tile_lbits
+  // (LC_TILE_LBITS / LC_TILE_WIDE), raised where the team would not fit the chip's workgroups
+  int team_lbits(int h) const {
+    int grid_log = 0;
+    while ((2 << grid_log) <= dgrid_b) ++grid_log;
+    const int lw = enc.live_max[h];
+    if (plan_lb[h] > 0 && plan_lb[h] < DENSE_LMAX) return plan_lb[h];  // team planner
+    const int want = lw >= wide_from ? std::min(wide_lbits, tile_lbits) : tile_lbits;
+    return std::min(DENSE_LMAX, std::max(lw - grid_log, std::min(want, lw - 1)));
+  }
+
   // Step streams for the dense closure-table kernels (format: dense.hpp). Eligible:
   // cas-register, <= DENSE_MAX_STATES register values, live width <= dense_maxw.
   int build_dense() {
@@ -420,6 +433,37 @@ struct lc_plan {
        : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
     }
     plan_teams(widths);
+    // LC_TEAM_ROT=r: a tile team's slots relabelled so its r lowest slots (the ones live in
+    // almost every step) become the top r team bits and the others move down r places. Slot
+    // labels are arbitrary (masks are sets), so the answer is unchanged; what changes is which
+    // tiles work in a step: with low slots as team bits every tile holds a share of every step,
+    // instead of tile 0 holding every step whole.
+    // Default (LC_TEAM_ROT unset): full rotation for teams whose tiles hold >= rot_min_lb local
+    // slots, where tile 0's share of every step is the chain (C4, lb 16: 1.85 s -> 0.90 s);
+    // narrower tiles (C2, lb 13: 35.4 -> 39.7 ms rotated) keep their narrow steps off the
+    // exchange.
+    if (team_rot != 0)
+      for (int h : dense_x) {
+        const int lw = enc.live_max[h], lb = team_lbits(h);
+        if (team_rot < 0 && lb < rot_min_lb) continue;
+        const int r = team_rot < 0 ? lw - lb : std::min(team_rot, lw - lb);
+        if (r <= 0) continue;
+        uint32_t perm[32];
+        for (int k = 0; k < 32; ++k) perm[k] = k < lw ? (uint32_t)(k < r ? lw - r + k : k - r) : (uint32_t)k;
+        uint32_t* w = words.data() + sbeg[h];
+        uint32_t* const e = words.data() + wcount[h + 1];
+        while (w < e) {
+          const uint32_t x = *w;
+          if (x & DENSE_OPW) {
+            *w = (x & ~0xffu) | perm[x & 31u];
+          } else {
+            uint32_t live = 0;
+            for (uint32_t m = x & DENSE_LIVE_MASK; m; m &= m - 1) live |= 1u << perm[__builtin_ctz(m)];
+            *w = live | (perm[(x >> DENSE_J_SHIFT) & 31u] << DENSE_J_SHIFT);
+          }
+          ++w;
+        }
+      }
     pool_block_us = 0, pool_mid_us = 0, pool_wave_us = 0;  // the BLOCK pool's planned work
     for (int h : dense_b) pool_block_us += est_block_us(widths[h]);
     if (dense_pipe & 128) for (int h : dense_m) pool_mid_us += est_mid_us(widths[h]) / 4.0;
@@ -475,13 +519,20 @@ struct lc_plan {
     return t;
   }
   double pool_block_us = 0, pool_mid_us = 0, pool_wave_us = 0;  // the planned pool's work (WG-us)
+  int team_rot = -1;       // LC_TEAM_ROT: tile-team slot rotation (build_dense; -1 auto)
+  int rot_min_lb = 16;     // LC_TEAM_ROT_LB: auto rotation from this tile size
   int mid_maxw = 14;       // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7)
-  double plan_k16 = 0.7;  // LC_PLAN_K: scales the team model's VALU term (r2x sweep with MID
-                          // histories in big workgroups: 0.6-0.7 best on C3)
+  // LC_PLAN_K: scales the team model's VALU term. The model was fitted on unrotated teams;
+  // rotated teams (auto from lb 16) spread every step over the tiles, so fewer tiles serve. A
+  // batch plan (many histories sharing the chip) is throughput-bound and wants them (r2rot4/5
+  // sweep on C3: 0.4-0.45 -> 11.7 ms, 0.7 -> 13.4-13.6); a plan of a few histories is their
+  // chain and keeps the unrotated fit's calibration (C2: 0.7 -> 35.5 ms, 0.4 -> 39.1 ms).
+  double plan_k16 = -1;  // < 0: 0.7 for <= 8 histories, else 0.45
   double est_team_us(const std::vector<uint8_t>& ws, int lb) const {
     double t = 0;
     for (uint8_t L : ws) {
-      t += 1.59 + 0.0043 * plan_k16 * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
+      const double k = plan_k16 > 0 ? plan_k16 : enc.n_hist <= 8 ? 0.7 : 0.45;
+      t += 1.59 + 0.0043 * k * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
       if (L > lb) t += 3.87 + 1.57 * (L - lb);
     }
     return t;
@@ -586,14 +637,7 @@ struct lc_plan {
     int used = 0;
     // local slots per tile: tile_lbits (<= DENSE_LMAX, the LDS tile), raised where the team
     // would not fit the chip's workgroups; a team larger than `cap` gets a launch of its own
-    int grid_log = 0;
-    while ((2 << grid_log) <= dgrid_b) ++grid_log;
-    auto lbits_of = [&](int h) {
-      const int lw = enc.live_max[h];
-      if (plan_lb[h] > 0 && plan_lb[h] < DENSE_LMAX) return plan_lb[h];  // team planner
-      const int want = lw >= wide_from ? std::min(wide_lbits, tile_lbits) : tile_lbits;
-      return std::min(DENSE_LMAX, std::max(lw - grid_log, std::min(want, lw - 1)));
-    };
+    auto lbits_of = [&](int h) { return team_lbits(h); };
     for (int h : dense_x) {
       const int g = 1 << (enc.live_max[h] - lbits_of(h));
       if (used + g > cap && !launches.back().empty()) {
