@@ -269,6 +269,7 @@ struct lc_plan {
     if ((e = getenv("LC_PLAN_K")) && atof(e) > 0) plan_k16 = atof(e);
     if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
     if ((e = getenv("LC_TEAM_ROT_LB"))) rot_min_lb = atoi(e);
+    if ((e = getenv("LC_BATCH_HIST"))) batch_hist = atoi(e);
     if ((e = getenv("LC_MID_MAXW")) && atoi(e) > DENSE_WAVE_LMAX && atoi(e) <= DENSE_MID_LMAX) mid_maxw = atoi(e);
     if ((e = getenv("LC_TILE_WIDE")) && strchr(e, ':')) {
       wide_from = atoi(e);
@@ -439,13 +440,20 @@ struct lc_plan {
     // tiles work in a step: with low slots as team bits every tile holds a share of every step,
     // instead of tile 0 holding every step whole.
     // Default (LC_TEAM_ROT unset): full rotation for teams whose tiles hold >= rot_min_lb local
-    // slots, where tile 0's share of every step is the chain (C4, lb 16: 1.85 s -> 0.90 s);
-    // narrower tiles (C2, lb 13: 35.4 -> 39.7 ms rotated) keep their narrow steps off the
-    // exchange.
+    // slots when the plan is a batch (throughput: rotated big tiles are the cheapest teams) or
+    // at least 40 % of the history's steps are wide anyway (C4, lb 16: 1.85 s -> 0.90 s). A
+    // chain plan's mostly-narrow histories keep their narrow steps on tile 0 alone, off the
+    // exchange (a C3 125-key share: 8.2 ms unrotated, 8.9 rotated), and so do narrower tiles
+    // (C2, lb 13: 35.4 ms, 39.7 rotated).
     if (team_rot != 0)
       for (int h : dense_x) {
         const int lw = enc.live_max[h], lb = team_lbits(h);
-        if (team_rot < 0 && lb < rot_min_lb) continue;
+        if (team_rot < 0) {  // auto: a batch plan's big-tile teams, or mostly-wide histories
+          int wide = 0;
+          for (uint8_t L : widths[h]) wide += L > lb;
+          const bool mostly_wide = 10 * wide >= 4 * (int)widths[h].size();
+          if (lb < rot_min_lb || !(batch_plan() || mostly_wide)) continue;
+        }
         const int r = team_rot < 0 ? lw - lb : std::min(team_rot, lw - lb);
         if (r <= 0) continue;
         uint32_t perm[32];
@@ -527,11 +535,17 @@ struct lc_plan {
   // batch plan (many histories sharing the chip) is throughput-bound and wants them (r2rot4/5
   // sweep on C3: 0.4-0.45 -> 11.7 ms, 0.7 -> 13.4-13.6); a plan of a few histories is their
   // chain and keeps the unrotated fit's calibration (C2: 0.7 -> 35.5 ms, 0.4 -> 39.1 ms).
-  double plan_k16 = -1;  // < 0: 0.7 for <= 8 histories, else 0.45
+  double plan_k16 = -1;  // < 0: 0.45 for a batch plan, else 0.7
+  // A batch plan (LC_BATCH_HIST: more than 400 histories, e.g. C3 on 1-2 GPUs) fills the chip,
+  // so the launch is throughput-bound; fewer histories leave workgroups idle and the launch is
+  // its slowest chain (r2rot6-8: C3 1000 keys 11.8 ms batch / 16.2 unrotated; a 250-key share
+  // 8.2-9.5 ms as a chain plan, 9.6-9.9 as a batch plan).
+  int batch_hist = 400;
+  bool batch_plan() const { return enc.n_hist > batch_hist; }
   double est_team_us(const std::vector<uint8_t>& ws, int lb) const {
     double t = 0;
     for (uint8_t L : ws) {
-      const double k = plan_k16 > 0 ? plan_k16 : enc.n_hist <= 8 ? 0.7 : 0.45;
+      const double k = plan_k16 > 0 ? plan_k16 : batch_plan() ? 0.45 : 0.7;
       t += 1.59 + 0.0043 * k * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
       if (L > lb) t += 3.87 + 1.57 * (L - lb);
     }

@@ -578,6 +578,22 @@ def test_gpu_dense_tile_teams_small_tiles(lbits, monkeypatch):
     p.close()
 
 
+@pytest.mark.parametrize("rot,lbits", [("1", "14"), ("3", "13"), ("9", "15"), ("9", None)])
+def test_gpu_dense_tile_teams_rotated(rot, lbits, monkeypatch):
+    """LC_TEAM_ROT: a tile team's lowest slots relabelled as its team bits (every tile holds a
+    share of every step). Slot labels are arbitrary, so every answer stays the oracle's."""
+    monkeypatch.setenv("LC_TEAM_ROT", rot)
+    if lbits:
+        monkeypatch.setenv("LC_TILE_LBITS", lbits)
+    h, widths, exp = _wide_batch()
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    got = p.results()
+    for k in range(h.n_hist):
+        _cmp(got, exp[k], k, f"rotated {rot} lbits={lbits} w={widths[k]}")
+    p.close()
+
+
 @pytest.mark.parametrize("lbits", [None, "15"])
 def test_gpu_dense_tile_teams_pipelined(lbits, monkeypatch):
     """LC_PIPE bit 2: tile teams overlap steps (team_pipe: per-step mirror slots, super-layer
