@@ -411,15 +411,10 @@ def main():
             ts.append(time.perf_counter() - t0)
         ts.sort()
         med = ts[len(ts) // 2]
-        # lc_check's own setup split (a warm lc_plan_create, as each lc_check makes one)
-        warm = _lib.Plan(kind, 0, h, device=local)
-        wst = warm.stats()
-        warm.close()
+        # (lc_check keeps one plan per device; LC_PHASES=1 prints each call's setup split)
         e2e = {"ms_per_check": med * 1e3, "value": h.n_ops() / med, "unit": "history ops/s",
                "reps": args.e2e_reps, "what": "lc_check from host arrays (encode + H2D + search "
                "+ D2H), this rank's histories",
-               "plan_create_phases_ms": {k[len("create_"):]: round(wst[k], 3) for k in wst
-                                         if k.startswith("create_")},
                "first_plan_create_phases_ms": phases}
 
     if dist:
