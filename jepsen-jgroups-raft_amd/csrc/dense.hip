@@ -134,6 +134,33 @@ struct HbmTab {
   }
 };
 
+// Tagged mirror words (LC_PIPE bit 8): word i of a mirror slot is two 8-byte granules
+// {data half, tag}, each single-copy atomic, so a reader polls the data itself until both tags
+// name the step it wants (MI355X_MICROARCH "handoff-1to1": data-tagged 8-byte granules). The
+// producer then needs neither a store drain nor a token on the hand-off path.
+struct TagTab {
+  static __device__ __forceinline__ void st(uint64_t* slot, uint32_t i, uint64_t v, uint32_t tag) {
+    HbmTab::st(&slot[2 * i], ((uint64_t)tag << 32) | (uint32_t)v);
+    HbmTab::st(&slot[2 * i + 1], ((uint64_t)tag << 32) | (uint32_t)(v >> 32));
+  }
+  // both granules of word i once they carry `tag`; a 20 s watchdog raises *abort (then 0)
+  static __device__ __forceinline__ uint64_t ld(const uint64_t* slot, uint32_t i, uint32_t tag, int32_t* abort) {
+    uint64_t a = HbmTab::ld(&slot[2 * i]), b = HbmTab::ld(&slot[2 * i + 1]);
+    if ((uint32_t)(a >> 32) == tag && (uint32_t)(b >> 32) == tag) return (uint32_t)a | (b << 32);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (long spins = 1;; ++spins) {
+      __builtin_amdgcn_s_sleep(1);
+      a = HbmTab::ld(&slot[2 * i]);
+      b = HbmTab::ld(&slot[2 * i + 1]);
+      if ((uint32_t)(a >> 32) == tag && (uint32_t)(b >> 32) == tag) return (uint32_t)a | (b << 32);
+      if ((spins & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull || ld_agent(abort))) {
+        st_agent(abort, 1);
+        return 0;
+      }
+    }
+  }
+};
+
 
 // Pulls of word w over its hi bits from the finalized words one hi bit below (LDS table B):
 // the bulk of a word's closure, needing nothing from other tiles. BATCH bits at a time: the
@@ -1068,9 +1095,14 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   const uint32_t lmask = (1u << lb) - 1;
   unsigned long long* const flags = p.flags + base;
   uint32_t* const anyv = p.team_any + p.team_any_off[team];
+  // LC_PIPE bit 8: tagged mirror words (two granules per word, TagTab): readers poll the data,
+  // no token waits before a super-layer, no store drain after it (tokens remain for credits)
+  const bool tagged = (p.pipe & 256) != 0;
+  const int mshift = HSOLO + (tagged ? 1 : 0);
   auto mirror = [&](int r, int t) {
-    return p.mirror + (((size_t)(base + r) * MRING + (size_t)(t % MRING)) << HSOLO);
+    return p.mirror + (((size_t)(base + r) * MRING + (size_t)(t % MRING)) << mshift);
   };
+  auto tag_of = [&](int t) { return p.mirror_tag + (uint32_t)t + 1u; };
   const int ns = p.nsteps[h];
   // LC_DEBUG phase cycles: pred/X waits, segments, publish + token, credit waits, -, super-layers
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
@@ -1138,7 +1170,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
       pm_l = lteam_l == 0 ? 0u : tile_j ? (1u << jt) : ((uint32_t)rank & lteam_l);
       if (h1.y >= lb && !((uint32_t)rank & (h0.y >> lb))) xs_l = rank | (1 << (h1.y - lb));
     }
-    if (__any(pm_l != 0 || xs_l >= 0)) {  // wait for the tiles this super-layer reads
+    if (!tagged && __any(pm_l != 0 || xs_l >= 0)) {  // wait for the tiles this super-layer reads
       if (decoder) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         long spins = 0;
@@ -1205,13 +1237,21 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         const bool fx = !tile_fresh && !(w & fresh_hi);
         // HBM loads first (X from tile xs, one pull per predecessor tile), used after
         uint64_t xv = 0, pv[TB];
-        if (fx && xs >= 0) xv = HbmTab::ld(mirror(xs, t - 1) + mp + r);
         // pulls from the tiles one team bit below: none for masks holding a local j (never
         // expanded); a tile holding j takes only T_j of r \ j
         const bool pl = tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u));
+        if (tagged) {
+          if (fx && xs >= 0) xv = TagTab::ld(mirror(xs, t - 1), mp + r, tag_of(t - 1), p.abort);
 #pragma unroll
-        for (int b = 0; b < TB; ++b)
-          pv[b] = (pl && ((pmask >> b) & 1u)) ? HbmTab::ld(mirror(rank ^ (1 << b), t) + mo + r) : 0ull;
+          for (int b = 0; b < TB; ++b)
+            pv[b] = (pl && ((pmask >> b) & 1u)) ? TagTab::ld(mirror(rank ^ (1 << b), t), mo + r, tag_of(t), p.abort)
+                                                 : 0ull;
+        } else {
+          if (fx && xs >= 0) xv = HbmTab::ld(mirror(xs, t - 1) + mp + r);
+#pragma unroll
+          for (int b = 0; b < TB; ++b)
+            pv[b] = (pl && ((pmask >> b) & 1u)) ? HbmTab::ld(mirror(rank ^ (1 << b), t) + mo + r) : 0ull;
+        }
         uint64_t X = xs >= 0 ? (xv & keep_lo) : (fx && jp < lb) ? pipe_x(B, w, 0u, jp, keep_lo) : 0ull;
         uint64_t R = tile_j ? 0ull : pull_hi<4>(B, zero, w, j, H, ops, foldm);
 #pragma unroll
@@ -1220,7 +1260,10 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         if (!tile_j) R = close_in_word(X, w, live_loc, j, ops, foldm, R);
         const uint64_t nv = X | R;
         B[w] = nv;
-        if (wide) HbmTab::st(mirror(rank, t) + mo + r, nv);
+        if (wide) {
+          if (tagged) TagTab::st(mirror(rank, t), mo + r, nv, tag_of(t));
+          else HbmTab::st(mirror(rank, t) + mo + r, nv);
+        }
         expl += (uint32_t)__popcll(R);
         if (t > 0) st_fout += (uint32_t)__popcll(X);
         if (X) st->anyx = 1;
@@ -1348,7 +1391,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
       }
     }
     if (timed) ph[1] += now() - tp, tp = now();
-    if (wide_any) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    if (wide_any && !tagged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
     __syncthreads();
     if (tid == 0) st_agent(&flags[rank], (unsigned long long)(s + 1));
     if (timed) ph[2] += now() - tp, ph[5] += 1;
@@ -1370,7 +1413,9 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         for (uint32_t r = (uint32_t)tid; r < nq; r += 1024u) {
           const uint32_t w = p.words[o + r];
           if (w & ~live_hi) continue;
-          const uint64_t X = xsrc ? HbmTab::ld(xsrc + mo + r) : pipe_x(B, w, 0u, jl, ~0ull);
+          const uint64_t X = !xsrc ? pipe_x(B, w, 0u, jl, ~0ull)
+                             : tagged ? TagTab::ld(xsrc, mo + r, tag_of(ns - 1), p.abort)
+                                      : HbmTab::ld(xsrc + mo + r);
           st_fout += (uint32_t)__popcll(X);
           nzx |= X;
         }

@@ -76,6 +76,7 @@ struct DenseParams {
   int32_t n_w;                  // big kernel: WAVE histories its waves run after the BLOCK
   const int32_t* order_w;       // queue (0: dense_wave_kernel runs them)
   int32_t* queue_w;
+  uint32_t mirror_tag;          // tagged mirrors (LC_PIPE bit 8): this launch's tag base
   int32_t mid_first;            // big kernel, LC_PIPE bit 7: BLOCK-pool workgroups (just below the
                                 // WAVE-first ones) that start on the MID queue
   int32_t pipe;                 // bit 3: tile teams without per-step team barriers;

@@ -143,8 +143,10 @@ struct lc_plan {
   // MID teams for widths 12..14 (needs bit 0); bit 5 = one pass per running segment (r1 form;
   // default: segments packed over the team); bit 6 = WAVE histories on the big kernel's waves
   // (no dense_wave_kernel); bit 7 = MID histories (widths 12..mid_maxw) as 4-wave teams inside
-  // big workgroups (no dense_mid_kernel). Default 207 = 1|2|4|8|64|128, with the team planner.
-  int dense_pipe = 207;
+  // big workgroups (no dense_mid_kernel); bit 8 = tagged tile-team mirror words (readers poll
+  // the data; by default chain plans only). Default 463 = 1|2|4|8|64|128|256, with the planner.
+  int dense_pipe = 463;
+  bool pipe_env = false;  // LC_PIPE given: its bits as they are
   std::vector<int> plan_lb;  // team planner: local slots per tile (0: not a team)
   bool plan_off = false;     // LC_TEAM_PLAN=0: every wide history keeps 17-bit tiles
   hipStream_t stream2 = nullptr, stream3 = nullptr;
@@ -264,7 +266,7 @@ struct lc_plan {
     if ((e = getenv("LC_TILE_WGS")) && atoi(e) > 0) tile_cap = atoi(e);
     if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
-    if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e);
+    if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e), pipe_env = true;
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
     if ((e = getenv("LC_PLAN_K")) && atof(e) > 0) plan_k16 = atof(e);
     if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
@@ -527,6 +529,7 @@ struct lc_plan {
     return t;
   }
   double pool_block_us = 0, pool_mid_us = 0, pool_wave_us = 0;  // the planned pool's work (WG-us)
+  uint32_t mirror_seq = 0;  // tagged mirrors: launches since the buffer was last zeroed
   int team_rot = -1;       // LC_TEAM_ROT: tile-team slot rotation (build_dense; -1 auto)
   int rot_min_lb = 16;     // LC_TEAM_ROT_LB: auto rotation from this tile size
   int mid_maxw = 14;       // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7)
@@ -701,11 +704,21 @@ struct lc_plan {
     for (size_t l = 0; l < launches.size(); ++l)
       for (int8_t t : l_bits[l])
         if (t > ((dense_pipe & DENSE_PIPE_SERIAL_SEGS) ? DENSE_TEAM_MAXB_SERIAL : DENSE_TEAM_MAXB)) pipe_mode &= ~4;
+    // tagged mirror words (bit 8): packed pipelined teams only; a tag holds the step in its
+    // low 20 bits above a launch sequence, so histories of 2^20 steps or more use tokens
+    if (!(pipe_mode & 4) || (pipe_mode & DENSE_PIPE_SERIAL_SEGS)) pipe_mode &= ~256;
+    // by default only chain plans: a batch plan's teams are throughput-bound and the doubled
+    // mirror traffic costs it ~2 % (C3 12.2 -> 12.5 ms), while C2 / C4 gain 6 % / 10 % (r2tag)
+    if (!pipe_env && batch_plan()) pipe_mode &= ~256;
+    for (int h : dense_x)
+      if (enc.n_steps(h) >= (1 << 20) - 1) pipe_mode &= ~256;
     p.pipe = pipe_mode;
     if (max_wgs) {
       const size_t slots = (pipe_mode & 4) ? DENSE_MRING : 2;  // 2: the per-step loop's buffers
+      const size_t mbytes = (max_wgs * slots << (DENSE_LMAX - 3)) * 8 * ((pipe_mode & 256) ? 2 : 1);
       HIP_TRY(d_tdone.ensure(max_wgs * 8));
-      HIP_TRY(d_mirror.ensure((max_wgs * slots << (DENSE_LMAX - 3)) * 8));
+      if (mbytes > d_mirror.bytes || !d_mirror.p) mirror_seq = 0;  // fresh buffer: zeroed below
+      HIP_TRY(d_mirror.ensure(mbytes));
       HIP_TRY(d_tany.ensure(std::max<size_t>(max_anyw, 1) * 4));
       HIP_TRY(d_tanyoff.ensure(max_teams * 4));
       HIP_TRY(d_tflags.ensure(max_wgs * 8));
@@ -790,6 +803,11 @@ struct lc_plan {
         q.team_lbits = d_tlbits.as<int8_t>();
         q.team_hist = d_thist.as<int32_t>();
         q.mirror = d_mirror.as<uint64_t>();
+        if (q.pipe & 256) {  // a fresh tag range per launch; the buffer is zeroed every 4096
+          if ((mirror_seq & 0xfffu) == 0) HIP_TRY(hipMemsetAsync(d_mirror.p, 0, d_mirror.bytes, stream));
+          q.mirror_tag = (mirror_seq & 0xfffu) << 20;
+          ++mirror_seq;
+        }
         q.flags = d_tflags.as<unsigned long long>();
         q.ctl = d_ctl.p;
         q.abort = d_abort.as<int32_t>();

@@ -578,11 +578,14 @@ def test_gpu_dense_tile_teams_small_tiles(lbits, monkeypatch):
     p.close()
 
 
+@pytest.mark.parametrize("pipe", ["207", "463"], ids=["tokens", "tagged"])
 @pytest.mark.parametrize("rot,lbits", [("1", "14"), ("3", "13"), ("9", "15"), ("9", None)])
-def test_gpu_dense_tile_teams_rotated(rot, lbits, monkeypatch):
+def test_gpu_dense_tile_teams_rotated(rot, lbits, pipe, monkeypatch):
     """LC_TEAM_ROT: a tile team's lowest slots relabelled as its team bits (every tile holds a
-    share of every step). Slot labels are arbitrary, so every answer stays the oracle's."""
+    share of every step). Slot labels are arbitrary, so every answer stays the oracle's. With
+    LC_PIPE 463 the team mirrors are tagged words polled by their readers (no tokens)."""
     monkeypatch.setenv("LC_TEAM_ROT", rot)
+    monkeypatch.setenv("LC_PIPE", pipe)
     if lbits:
         monkeypatch.setenv("LC_TILE_LBITS", lbits)
     h, widths, exp = _wide_batch()
