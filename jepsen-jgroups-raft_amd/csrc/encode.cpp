@@ -2,6 +2,7 @@
 #include "encode.hpp"
 
 #include <algorithm>
+#include <climits>
 #include <thread>
 #include <unordered_map>
 
@@ -114,45 +115,58 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
   ops.clear();
   std::vector<int32_t>& op_of = sc.op_of;
   op_of.assign(e - b, -1);
-  // process -> its outstanding op: open addressing over a power-of-two table (processes are
-  // arbitrary int32; a history has at most one per entry)
-  const size_t cap = (size_t)1 << (64 - __builtin_clzll((unsigned long long)(e - b) | 15));
-  const size_t pmask = cap * 2 - 1;
-  sc.pkey.resize(cap * 2);
-  sc.pval.assign(cap * 2, -2);
-  int32_t* pkey = sc.pkey.data();
-  int32_t* pval = sc.pval.data();
-  auto slot_of = [&](int32_t proc) -> int32_t& {
-    size_t k = ((uint32_t)proc * 0x9E3779B1u) & pmask;
-    while (pval[k] != -2 && pkey[k] != proc) k = (k + 1) & pmask;
-    if (pval[k] == -2) pkey[k] = proc, pval[k] = -1;
-    return pval[k];
-  };
+  // process -> its outstanding op (-1: none): a direct table over [pmin, pmax] when the process
+  // ids are dense (Jepsen's are small integers), else open addressing over a power-of-two table
+  // (processes are arbitrary int32; a history has at most one per entry)
+  int32_t pmin = INT32_MAX, pmax = INT32_MIN;
+  for (int64_t i = b; i < e; ++i) pmin = std::min(pmin, a.process[i]), pmax = std::max(pmax, a.process[i]);
   int64_t n_ok = 0;
-  for (int64_t i = b; i < e; ++i) {
-    int8_t t = a.type[i];
-    int32_t& cur = slot_of(a.process[i]);
-    if (t == T_INVOKE) {
-      if (cur >= 0) return fail(LC_H_MALFORMED, "process invoked while an op was outstanding");
-      cur = (int32_t)ops.size();
-      op_of[i - b] = cur;
-      ops.push_back(Op{i, a.v0[i], a.v1[i], -1, a.f[i], a.vflags[i], 0});
-    } else if (t == T_OK || t == T_FAIL || t == T_INFO) {
-      if (cur < 0) return fail(LC_H_MALFORMED, "completion without an outstanding invocation");
-      Op& op = ops[cur];
-      op.status = t;
-      if (t == T_OK) {  // fold the completion's value into the invocation
-        op.vflags = a.vflags[i];
-        op.v0 = a.v0[i];
-        op.v1 = a.v1[i];
-        n_ok++;
+  const char* bad = nullptr;
+  auto pair_all = [&](auto&& slot_of) {
+    for (int64_t i = b; i < e; ++i) {
+      const int8_t t = a.type[i];
+      int32_t& cur = slot_of(a.process[i]);
+      if (t == T_INVOKE) {
+        if (cur >= 0) return void(bad = "process invoked while an op was outstanding");
+        cur = (int32_t)ops.size();
+        op_of[i - b] = cur;
+        ops.push_back(Op{i, a.v0[i], a.v1[i], -1, a.f[i], a.vflags[i], 0});
+      } else if (t == T_OK || t == T_FAIL || t == T_INFO) {
+        if (cur < 0) return void(bad = "completion without an outstanding invocation");
+        Op& op = ops[cur];
+        op.status = t;
+        if (t == T_OK) {  // fold the completion's value into the invocation
+          op.vflags = a.vflags[i];
+          op.v0 = a.v0[i];
+          op.v1 = a.v1[i];
+          n_ok++;
+        }
+        op_of[i - b] = cur;
+        cur = -1;
+      } else {
+        return void(bad = "unknown :type");
       }
-      op_of[i - b] = cur;
-      cur = -1;
-    } else {
-      return fail(LC_H_MALFORMED, "unknown :type");
     }
+  };
+  if (e > b && (int64_t)pmax - pmin < 4 * (e - b) + 1024) {
+    sc.pval.assign((size_t)((int64_t)pmax - pmin + 1), -1);
+    int32_t* pval = sc.pval.data();
+    pair_all([&](int32_t proc) -> int32_t& { return pval[(int64_t)proc - pmin]; });
+  } else {
+    const size_t cap = (size_t)1 << (64 - __builtin_clzll((unsigned long long)(e - b) | 15));
+    const size_t pmask = cap * 2 - 1;
+    sc.pkey.resize(cap * 2);
+    sc.pval.assign(cap * 2, -2);  // -2: empty slot
+    int32_t* pkey = sc.pkey.data();
+    int32_t* pval = sc.pval.data();
+    pair_all([&](int32_t proc) -> int32_t& {
+      size_t k = ((uint32_t)proc * 0x9E3779B1u) & pmask;
+      while (pval[k] != -2 && pkey[k] != proc) k = (k + 1) & pmask;
+      if (pval[k] == -2) pkey[k] = proc, pval[k] = -1;
+      return pval[k];
+    });
   }
+  if (bad) return fail(LC_H_MALFORMED, bad);
   o.n_ops = (int64_t)ops.size();
   // ---- cas-register memo: value -> state id (id 0 = nil), ids in first-appearance order over
   // the values the register can hold; a linear scan while it has taken few values, then a map
@@ -186,15 +200,25 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
   // ---- RETURN steps with slot assignment (lowest free slot first), operands computed at each
   // invocation. Error precedence: a model error anywhere, then > 65535 register values, then
   // > 63 pending ops.
-  o.step_slot.reserve(n_ok);
-  o.step_ninv.reserve(n_ok);
-  o.step_cmp_idx.reserve(n_ok);
-  o.step_inv_idx.reserve(n_ok);
-  o.inv_slot.reserve(ops.size());
-  o.inv_kind.reserve(ops.size());
-  o.inv_a.reserve(ops.size());
-  o.inv_b.reserve(ops.size());
-  o.inv_index.reserve(ops.size());
+  o.step_slot.resize(n_ok);
+  o.step_ninv.resize(n_ok);
+  o.step_cmp_idx.resize(n_ok);
+  o.step_inv_idx.resize(n_ok);
+  o.inv_slot.resize(ops.size());
+  o.inv_kind.resize(ops.size());
+  o.inv_a.resize(ops.size());
+  o.inv_b.resize(ops.size());
+  o.inv_index.resize(ops.size());
+  uint8_t* const s_slot = o.step_slot.data();
+  int64_t* const s_ninv = o.step_ninv.data();
+  int64_t* const s_cmp = o.step_cmp_idx.data();
+  int64_t* const s_inv = o.step_inv_idx.data();
+  uint8_t* const i_slot = o.inv_slot.data();
+  uint8_t* const i_kind = o.inv_kind.data();
+  int64_t* const i_a = o.inv_a.data();
+  int64_t* const i_b = o.inv_b.data();
+  int64_t* const i_index = o.inv_index.data();
+  int64_t ns = 0, ni = 0;
   const char* wide = nullptr;
   uint64_t used = 0;
   int64_t ninv_cur = 0;
@@ -216,25 +240,32 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
         wide = "more than 63 pending ops";
         continue;
       }
-      const int s = __builtin_ctzll(~used);
-      used |= 1ull << s;
-      op.slot = (uint8_t)s;
+      const int sl = __builtin_ctzll(~used);
+      used |= 1ull << sl;
+      op.slot = (uint8_t)sl;
       o.live_max = std::max(o.live_max, 64 - __builtin_clzll(used));
-      o.inv_slot.push_back((uint8_t)s);
-      o.inv_kind.push_back(kind);
-      o.inv_a.push_back(oa);
-      o.inv_b.push_back(ob);
-      o.inv_index.push_back(IDX(op.inv_pos));
+      i_slot[ni] = (uint8_t)sl;
+      i_kind[ni] = kind;
+      i_a[ni] = oa;
+      i_b[ni] = ob;
+      i_index[ni] = IDX(i);  // (the invocation entry itself)
+      ++ni;
       ninv_cur++;
     } else if (t == T_OK && !wide) {
-      o.step_slot.push_back(op.slot);
-      o.step_ninv.push_back(ninv_cur);
-      o.step_cmp_idx.push_back(IDX(i));
-      o.step_inv_idx.push_back(IDX(op.inv_pos));
+      s_slot[ns] = op.slot;
+      s_ninv[ns] = ninv_cur;
+      s_cmp[ns] = IDX(i);
+      s_inv[ns] = IDX(op.inv_pos);
+      ++ns;
       ninv_cur = 0;
       used &= ~(1ull << op.slot);
     }
   }
+  o.step_slot.resize(ns);
+  o.step_ninv.resize(ns);
+  o.step_cmp_idx.resize(ns);
+  o.step_inv_idx.resize(ns);
+  o.inv_slot.resize(ni);  // (trimmed below to the invocations before the last RETURN)
   if (model == LC_MODEL_CAS_REGISTER) {
     o.n_states = (int32_t)o.state_val.size() + 1;
     if (o.n_states > 65535) {
