@@ -1,0 +1,8 @@
+set -o pipefail
+o=gpurun_out/r2pl; mkdir -p $o
+for sh in 0/4 1/4 2/4 3/4 0/8 1/8 2/8 3/8 4/8 5/8 6/8 7/8 0/2 1/2; do
+n=$(echo $sh | tr / _)
+timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu --e2e-reps 0 --emulate $sh > $o/s${n}.json 2> /dev/null || exit 1
+done
+timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu --e2e-reps 0 > $o/c3.json 2> /dev/null || exit 1
+echo done
