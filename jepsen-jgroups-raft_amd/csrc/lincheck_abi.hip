@@ -432,7 +432,7 @@ struct lc_plan {
       const int lw = enc.live_max[h];
       // MID teams (several per CU) take the narrower BLOCK histories when BLOCK steps are pipelined
       (lw <= DENSE_WAVE_LMAX ? dense_w
-       : ((dense_pipe & 129) == 129 ? lw <= mid_maxw : lw <= DENSE_MID_LMAX && (dense_pipe & 17) == 17) ? dense_m
+       : ((dense_pipe & 129) == 129 ? lw <= mid_width() : lw <= DENSE_MID_LMAX && (dense_pipe & 17) == 17) ? dense_m
        : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
     }
     plan_teams(widths);
@@ -532,13 +532,18 @@ struct lc_plan {
   uint32_t mirror_seq = 0;  // tagged mirrors: launches since the buffer was last zeroed
   int team_rot = -1;       // LC_TEAM_ROT: tile-team slot rotation (build_dense; -1 auto)
   int rot_min_lb = 16;     // LC_TEAM_ROT_LB: auto rotation from this tile size
-  int mid_maxw = 14;       // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7)
+  // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7); by default 14 for
+  // a batch plan (four per CU is the cheaper throughput) and 12 for a chain plan, where a MID
+  // team's longer step (w14: 7.7 us against 4.9 as a BLOCK team) becomes a chain of its own
+  // (r2cd: 4-way shares 9.92 -> 9.67 ms at the slowest rank)
+  int mid_maxw = 0;
+  int mid_width() const { return mid_maxw > 0 ? mid_maxw : batch_plan() ? 14 : 12; }
   // LC_PLAN_K: scales the team model's VALU term. The model was fitted on unrotated teams;
   // rotated teams (auto from lb 16) spread every step over the tiles, so fewer tiles serve. A
   // batch plan (many histories sharing the chip) is throughput-bound and wants them (r2rot4/5
   // sweep on C3: 0.4-0.45 -> 11.7 ms, 0.7 -> 13.4-13.6); a plan of a few histories is their
-  // chain and keeps the unrotated fit's calibration (C2: 0.7 -> 35.5 ms, 0.4 -> 39.1 ms).
-  double plan_k16 = -1;  // < 0: 0.45 for a batch plan, else 0.7
+  // chain and keeps a higher factor (C2: 0.7 -> 35.5 ms, 0.4 -> 39.1 ms; rank shares: 1.0, r2cd).
+  double plan_k16 = -1;  // < 0: 0.45 for a batch plan, else 1.0 (r2cd)
   // A batch plan (LC_BATCH_HIST: more than 400 histories, e.g. C3 on 1-2 GPUs) fills the chip,
   // so the launch is throughput-bound; fewer histories leave workgroups idle and the launch is
   // its slowest chain (r2rot6-8: C3 1000 keys 11.8 ms batch / 16.2 unrotated; a 250-key share
@@ -548,7 +553,7 @@ struct lc_plan {
   double est_team_us(const std::vector<uint8_t>& ws, int lb) const {
     double t = 0;
     for (uint8_t L : ws) {
-      const double k = plan_k16 > 0 ? plan_k16 : batch_plan() ? 0.45 : 0.7;
+      const double k = plan_k16 > 0 ? plan_k16 : batch_plan() ? 0.45 : 1.0;
       t += 1.59 + 0.0043 * k * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
       if (L > lb) t += 3.87 + 1.57 * (L - lb);
     }
