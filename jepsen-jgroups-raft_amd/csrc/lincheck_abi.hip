@@ -544,11 +544,11 @@ struct lc_plan {
   // sweep on C3: 0.4-0.45 -> 11.7 ms, 0.7 -> 13.4-13.6); a plan of a few histories is their
   // chain and keeps a higher factor (C2: 0.7 -> 35.5 ms, 0.4 -> 39.1 ms; rank shares: 1.0, r2cd).
   double plan_k16 = -1;  // < 0: 0.45 for a batch plan, else 1.0 (r2cd)
-  // A batch plan (LC_BATCH_HIST: more than 400 histories, e.g. C3 on 1-2 GPUs) fills the chip,
+  // A batch plan (LC_BATCH_HIST: more than 600 histories, e.g. C3 on one GPU) fills the chip,
   // so the launch is throughput-bound; fewer histories leave workgroups idle and the launch is
   // its slowest chain (r2rot6-8: C3 1000 keys 11.8 ms batch / 16.2 unrotated; a 250-key share
   // 8.2-9.5 ms as a chain plan, 9.6-9.9 as a batch plan).
-  int batch_hist = 400;
+  int batch_hist = 600;  // (r2bh: a 500-key share as a chain plan: slowest rank 11.3 -> 10.9 ms)
   bool batch_plan() const { return enc.n_hist > batch_hist; }
   double est_team_us(const std::vector<uint8_t>& ws, int lb) const {
     double t = 0;
