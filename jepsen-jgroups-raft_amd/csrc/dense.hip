@@ -550,6 +550,11 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
 // t-1's post-return frontier: zero means step t-1 is the failing RETURN. An empty frontier
 // stays empty, so the steps started after a failure add no explored configs.
 constexpr int PIPE_SERIAL_SEGS = DENSE_PIPE_SERIAL_SEGS;
+// DenseParams.pipe bit 9: double-buffered tables. Step t works on table t & 1 and reads its X
+// from the other one, so the WAR hazard that makes a step wait two super-layers for its
+// predecessor disappears when the predecessor returned an in-word slot (jp < 3): step t's layer
+// q then needs only step t-1's layer q (the same words), and may run one super-layer after it.
+constexpr int PIPE_DBL = DENSE_PIPE_DBL;
 constexpr int PIPE_OPN = 26;  // op-table entries per step: OP_PAD + slots 0..24 (team slots), + the pull batches' tail
 struct __attribute__((aligned(16))) PipeStep {
   OpSel ops[PIPE_OPN];  // slot k at ops[OP_PAD + k]; every entry initialised
@@ -614,7 +619,7 @@ __device__ __forceinline__ T rdl(T v, int l) {
 // ("segments") and the next start all come from that view by ballots and readlanes.
 // SUB: the team is TEAM/64 waves of a larger workgroup (big_mid_mode), synchronised through
 // its own LDS barrier words qb (s_barrier would stop every wave of the workgroup).
-template <int TEAM, int TLOG, int RING, bool SUB = false>
+template <int TEAM, int TLOG, int RING, bool SUB = false, int CAPW = (1 << (TLOG - 3))>
 __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, const uint64_t* zero,
                                              PipeStep* ring, int* sQ, unsigned long long* sExpl,
                                              const uint32_t* words_g, const uint32_t* wofs_g, const uint32_t* binom,
@@ -643,16 +648,21 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
     const int lmax = p.lmax[h];
     const int NW = lmax > 3 ? 1 << (lmax - 3) : 1;
     const int ns = p.nsteps[h];
-    for (int i = tt; i < NW; i += TEAM) B[i] = 0;
+    // double-buffered tables (PIPE_DBL) when two fit the team's LDS: step t on tab(t)
+    const bool dbl = (p.pipe & PIPE_DBL) && 2 * NW <= CAPW;
+    uint64_t* const B2 = dbl ? B + NW : B;
+    auto tab = [&](int t) { return (t & 1) ? B2 : B; };
+    const int ntab = dbl ? 2 * NW : NW;
+    for (int i = tt; i < ntab; i += TEAM) B[i] = 0;
     // a BLOCK history of width <= 16 leaves room in the LDS table for its own word list (the
     // 2^(lmax-3) words below the table's width, by popcount layer) and the layers' offsets:
     // the word index of a packed pass then comes from LDS, not from the global list
     const uint32_t* words = words_g;
     const uint32_t* wofs = wofs_g;
     if constexpr (TLOG == DENSE_LMAX && TEAM >= 256) {
-      if (lmax <= DENSE_LMAX - 1 && lmax > 3) {
+      if (lmax <= DENSE_LMAX - 1 && lmax > 3 && ntab + NW / 2 + 16 <= CAPW) {
         const int Hh = lmax - 3;
-        uint32_t* lw = reinterpret_cast<uint32_t*>(B + NW);
+        uint32_t* lw = reinterpret_cast<uint32_t*>(B + ntab);
         uint32_t* lo = lw + NW;
         if (tt <= Hh + 1) {
           uint32_t o = 0;
@@ -668,7 +678,8 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       }
     }
     tsync();
-    if (tt == 0) B[0] = 1;  // (cas-register) starts at nil: state id 0, nothing linearized
+    // (cas-register) starts at nil: state id 0, nothing linearized; step 0 reads tab(-1)
+    if (tt == 0) B2[0] = 1;
     StreamWin sw;
     int64_t pos = p.sbeg[h];
     if (ns > 0 && decoder) {
@@ -750,10 +761,11 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
           for (int k = 0; k < 3; ++k)
             if (fresh & (1u << k)) keep_lo &= keep64(k);
           const OpSel* ops = st->ops + OP_PAD;
-          const uint64_t X = pipe_x(B, w, fresh >> 3, c.y, keep_lo);
-          uint64_t R = pull_hi<4>(B, zero, w, c.x, c.z, ops, foldm);
+          uint64_t* const Bt = tab(t);
+          const uint64_t X = pipe_x(tab(t - 1), w, fresh >> 3, c.y, keep_lo);
+          uint64_t R = pull_hi<4>(Bt, zero, w, c.x, c.z, ops, foldm);
           R = close_in_word(X, w, live, c.x, ops, foldm, R);
-          B[w] = X | R;
+          Bt[w] = X | R;
           expl += (uint32_t)__popcll(R);
           if (t > 0) st_fout += (uint32_t)__popcll(X);
           if (X) st->anyx = 1;
@@ -789,10 +801,11 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
             if (fresh & (1u << k)) keep_lo &= keep64(k);
           PipeStep* st = &ring[t % RING];
           const OpSel* ops = st->ops + OP_PAD;
-          const uint64_t X = pipe_x(B, w, fresh >> 3, jp, keep_lo);
-          uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+          uint64_t* const Bt = tab(t);
+          const uint64_t X = pipe_x(tab(t - 1), w, fresh >> 3, jp, keep_lo);
+          uint64_t R = pull_hi<4>(Bt, zero, w, j, H, ops, foldm);
           R = close_in_word(X, w, live, j, ops, foldm, R);
-          B[w] = X | R;
+          Bt[w] = X | R;
           expl += (uint32_t)__popcll(R);
           if (t > 0) st_fout += (uint32_t)__popcll(X);
           if (X) st->anyx = 1;
@@ -818,15 +831,17 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
         const uint32_t live_hi = live >> 3, fresh_hi = fresh >> 3;
         PipeStep* st = &ring[t % RING];
         const OpSel* ops = st->ops + OP_PAD;
+        uint64_t* const Bt = tab(t);
+        const uint64_t* const Bp = tab(t - 1);
         uint64_t nzx = 0;
         for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)TEAM) {
           const uint32_t w = wn;
           if (r + TEAM < nq) wn = words[o + r + TEAM];
           if (w & ~live_hi) continue;
-          const uint64_t X = pipe_x(B, w, fresh_hi, jp, keep_lo);
-          uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+          const uint64_t X = pipe_x(Bp, w, fresh_hi, jp, keep_lo);
+          uint64_t R = pull_hi<4>(Bt, zero, w, j, H, ops, foldm);
           R = close_in_word(X, w, live, j, ops, foldm, R);
-          B[w] = X | R;
+          Bt[w] = X | R;
           expl += (uint32_t)__popcll(R);
           if (t > 0) st_fout += (uint32_t)__popcll(X);
           nzx |= X;
@@ -842,10 +857,12 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
         ++t_dec;
       }
       // ---- start the next decoded step at s + 1: two super-layers after its predecessor
-      // (one if that has a single layer), or at once if the predecessor retired
+      // (one if that has a single layer, or returned an in-word slot on double-buffered
+      // tables), or at once if the predecessor retired
       if (t_run < t_dec_old) {
         const int lp = t_run - 1 - t_ret_old;  // the predecessor's lane (< 0: retired)
-        const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(2, rdl(h1.z, lp) + 1);
+        const int gap = (dbl && lp >= 0 && rdl(h1.x, lp) < 3) ? 1 : 2;
+        const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h1.z, lp) + 1);
         if (ok) {
           if (tt == 0) ring[t_run % RING].start = s + 1;
           ++t_run;
@@ -869,7 +886,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       uint64_t nzx = 0;
       for (int w = tt; w < nwt; w += TEAM) {
         if ((uint32_t)w & ~(live >> 3)) continue;
-        const uint64_t X = pipe_x(B, (uint32_t)w, 0u, jl, ~0ull);
+        const uint64_t X = pipe_x(tab(ns - 1), (uint32_t)w, 0u, jl, ~0ull);
         st_fout += (uint32_t)__popcll(X);
         nzx |= X;
       }
@@ -1093,6 +1110,10 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   const int tid = threadIdx.x, lane = tid & 63;
   const bool decoder = tid < 64;
   const uint32_t lmask = (1u << lb) - 1;
+  // double-buffered tile tables (PIPE_DBL) when two fit the LDS table (lb <= 16)
+  const bool dbl = (p.pipe & PIPE_DBL) && lb <= DENSE_LMAX - 1;
+  uint64_t* const B2 = dbl ? B + (1 << (lb - 3)) : B;
+  auto tab = [&](int t) { return (t & 1) ? B2 : B; };
   unsigned long long* const flags = p.flags + base;
   uint32_t* const anyv = p.team_any + p.team_any_off[team];
   // LC_PIPE bit 8: tagged mirror words (two granules per word, TagTab): readers poll the data,
@@ -1109,7 +1130,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   auto now = []() { return __builtin_amdgcn_s_memrealtime(); };
   const bool timed = p.tstamps != nullptr;
   if (p.stamps && rank == 0 && tid == 0) p.stamps[4 * h] = now();
-  if (rank == 0 && tid == 0) B[0] = 1;  // (cas-register) starts at nil: state id 0
+  if (rank == 0 && tid == 0) B2[0] = 1;  // (cas-register) starts at nil: state id 0 (step 0 reads tab(-1))
   StreamWin sw;
   int64_t pos = p.sbeg[h];
   if (ns > 0 && decoder) {
@@ -1224,11 +1245,12 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         const uint32_t fresh_hi = (fresh & lmask) >> 3;
         PipeStep* st = &ring[t % RING];
         const OpSel* ops = st->ops + OP_PAD;
+        uint64_t* const Bt = tab(t);
         if (!wide && xs < 0) {  // a step on this tile alone (then tile 0, jp local): LDS only
-          const uint64_t X = pipe_x(B, w, fresh_hi, jp, keep_lo);
-          uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+          const uint64_t X = pipe_x(tab(t - 1), w, fresh_hi, jp, keep_lo);
+          uint64_t R = pull_hi<4>(Bt, zero, w, j, H, ops, foldm);
           R = close_in_word(X, w, live_loc, j, ops, foldm, R);
-          B[w] = X | R;
+          Bt[w] = X | R;
           expl += (uint32_t)__popcll(R);
           if (t > 0) st_fout += (uint32_t)__popcll(X);
           if (X) st->anyx = 1;
@@ -1252,14 +1274,14 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
           for (int b = 0; b < TB; ++b)
             pv[b] = (pl && ((pmask >> b) & 1u)) ? HbmTab::ld(mirror(rank ^ (1 << b), t) + mo + r) : 0ull;
         }
-        uint64_t X = xs >= 0 ? (xv & keep_lo) : (fx && jp < lb) ? pipe_x(B, w, 0u, jp, keep_lo) : 0ull;
-        uint64_t R = tile_j ? 0ull : pull_hi<4>(B, zero, w, j, H, ops, foldm);
+        uint64_t X = xs >= 0 ? (xv & keep_lo) : (fx && jp < lb) ? pipe_x(tab(t - 1), w, 0u, jp, keep_lo) : 0ull;
+        uint64_t R = tile_j ? 0ull : pull_hi<4>(Bt, zero, w, j, H, ops, foldm);
 #pragma unroll
         for (int b = 0; b < TB; ++b)
           if ((pmask >> b) & 1u) R |= transfer(ops[lb + b], (foldm >> (lb + b)) & 1u, pv[b]);
         if (!tile_j) R = close_in_word(X, w, live_loc, j, ops, foldm, R);
         const uint64_t nv = X | R;
-        B[w] = nv;
+        Bt[w] = nv;
         if (wide) {
           if (tagged) TagTab::st(mirror(rank, t), mo + r, nv, tag_of(t));
           else HbmTab::st(mirror(rank, t) + mo + r, nv);
@@ -1306,6 +1328,8 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
       const uint32_t live_hi = live_loc >> 3, fresh_hi = (fresh & lmask) >> 3;
       PipeStep* st = &ring[t % RING];
       const OpSel* ops = st->ops + OP_PAD;
+      uint64_t* const Bt = tab(t);
+      const uint64_t* const Bp = tab(t - 1);
       const uint64_t* xsrc = xs >= 0 ? mirror(xs, t - 1) + mp : nullptr;
       uint64_t* mine = mirror(rank, t) + mo;
       uint64_t nzx = 0;
@@ -1317,10 +1341,10 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
             const uint32_t w = wn[k];
             wn[k] = rn < nq ? p.words[o + rn] : ~0u;
             if (r >= nq || (w & ~live_hi)) continue;
-            const uint64_t X = tile_fresh ? 0ull : pipe_x(B, w, fresh_hi, jp, keep_lo);
-            uint64_t R = pull_hi<4>(B, zero, w, j, H, ops, foldm);
+            const uint64_t X = tile_fresh ? 0ull : pipe_x(Bp, w, fresh_hi, jp, keep_lo);
+            uint64_t R = pull_hi<4>(Bt, zero, w, j, H, ops, foldm);
             R = close_in_word(X, w, live_loc, j, ops, foldm, R);
-            B[w] = X | R;
+            Bt[w] = X | R;
             expl += (uint32_t)__popcll(R);
             if (t > 0) st_fout += (uint32_t)__popcll(X);
             nzx |= X;
@@ -1357,14 +1381,14 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
           if (!ok[k]) continue;
           const uint32_t w = wl[k], r = r0 + 1024u * k;
           uint64_t X = xv[k] & keep_lo;
-          if (!xsrc && !tile_fresh && !(w & fresh_hi) && jp < lb) X = pipe_x(B, w, 0u, jp, keep_lo);
-          uint64_t R = tile_j ? 0ull : pull_hi<4>(B, zero, w, j, H, ops, foldm);
+          if (!xsrc && !tile_fresh && !(w & fresh_hi) && jp < lb) X = pipe_x(Bp, w, 0u, jp, keep_lo);
+          uint64_t R = tile_j ? 0ull : pull_hi<4>(Bt, zero, w, j, H, ops, foldm);
 #pragma unroll
           for (int b = 0; b < TB; ++b)
             if ((pmask >> b) & 1u) R |= transfer(ops[lb + b], (foldm >> (lb + b)) & 1u, pv[k][b]);
           if (!tile_j) R = close_in_word(X, w, live_loc, j, ops, foldm, R);
           const uint64_t nv = X | R;
-          B[w] = nv;
+          Bt[w] = nv;
           if (wide) HbmTab::st(mine + r, nv);
           expl += (uint32_t)__popcll(R);
           if (t > 0) st_fout += (uint32_t)__popcll(X);
@@ -1383,7 +1407,8 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     }
     if (t_run < t_dec_old) {
       const int lp = t_run - 1 - t_ret_old;
-      const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(2, rdl(h1.z, lp) + 1);
+      const int gap = (dbl && lp >= 0 && rdl(h1.x, lp) < 3) ? 1 : 2;  // as in history_pipe
+      const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h1.z, lp) + 1);
       if (ok) {
         if (tid == 0) ring[t_run % RING].start = s + 1, ring[t_run % RING].pstart = last_start;
         last_start = s + 1;
@@ -1413,7 +1438,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         for (uint32_t r = (uint32_t)tid; r < nq; r += 1024u) {
           const uint32_t w = p.words[o + r];
           if (w & ~live_hi) continue;
-          const uint64_t X = !xsrc ? pipe_x(B, w, 0u, jl, ~0ull)
+          const uint64_t X = !xsrc ? pipe_x(tab(ns - 1), w, 0u, jl, ~0ull)
                              : tagged ? TagTab::ld(xsrc, mo + r, tag_of(ns - 1), p.abort)
                                       : HbmTab::ld(xsrc + mo + r);
           st_fout += (uint32_t)__popcll(X);
@@ -1435,14 +1460,15 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
 __device__ __forceinline__ void big_wave_mode(const DenseParams& p, uint64_t* sTab, const uint64_t* zero,
                                               const uint32_t* binom, int tid, unsigned long long& st_fout,
                                               unsigned long long& st_steps) {
-  constexpr int NWV = 16, HW = DENSE_WAVE_LMAX - 3, TABW = 1 << HW;
-  uint64_t* const tabs = sTab;                                         // NWV tables of TABW words
-  PipeStep* const rings = reinterpret_cast<PipeStep*>(sTab + NWV * TABW);  // NWV rings
+  // each wave's slice holds two tables of TABW words (PIPE_DBL)
+  constexpr int NWV = 16, HW = DENSE_WAVE_LMAX - 3, TABW = 1 << HW, SLW = 2 * TABW;
+  uint64_t* const tabs = sTab;                                         // NWV slices of SLW words
+  PipeStep* const rings = reinterpret_cast<PipeStep*>(sTab + NWV * SLW);  // NWV rings
   uint32_t* const words = reinterpret_cast<uint32_t*>(rings + NWV * WAVE_RING);  // HW-bit word list
   uint32_t* const wofs = words + TABW;                                 // its layer offsets
   int* const sQw = reinterpret_cast<int*>(wofs + 16);
   unsigned long long* const sEx = reinterpret_cast<unsigned long long*>(sQw + NWV);
-  static_assert((NWV * TABW) * 8 + NWV * WAVE_RING * sizeof(PipeStep) + TABW * 4 + 16 * 4 + NWV * 4 + NWV * 8 <=
+  static_assert((NWV * SLW) * 8 + NWV * WAVE_RING * sizeof(PipeStep) + TABW * 4 + 16 * 4 + NWV * 4 + NWV * 8 <=
                 (1 << (DENSE_LMAX - 3)) * 8, "wave mode fits the big table");
   __syncthreads();  // the table's previous users are done
   if (tid <= HW + 1) {
@@ -1461,8 +1487,8 @@ __device__ __forceinline__ void big_wave_mode(const DenseParams& p, uint64_t* sT
   DenseParams q = p;
   q.n = p.n_w, q.order = p.order_w, q.queue = p.queue_w;
   const int w = tid / 64;
-  history_pipe<64, DENSE_WAVE_LMAX, WAVE_RING>(q, tabs + w * TABW, zero, rings + w * WAVE_RING, &sQw[w], &sEx[w],
-                                               words, wofs, binom, tid & 63, st_fout, st_steps);
+  history_pipe<64, DENSE_WAVE_LMAX, WAVE_RING, false, SLW>(q, tabs + w * SLW, zero, rings + w * WAVE_RING, &sQw[w],
+                                                          &sEx[w], words, wofs, binom, tid & 63, st_fout, st_steps);
   __syncthreads();
 }
 

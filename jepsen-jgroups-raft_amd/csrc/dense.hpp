@@ -25,6 +25,7 @@ constexpr int DENSE_MRING = 32;      // mirror slots per tile (pipelined tile te
 constexpr int DENSE_TEAM_MAXB = 8;   // team bits of a pipelined tile team (packed segments)
 constexpr int DENSE_TEAM_MAXB_SERIAL = 5;  // ... with serial segments
 constexpr int DENSE_PIPE_SERIAL_SEGS = 32;  // DenseParams.pipe bit 5: one pass per segment
+constexpr int DENSE_PIPE_DBL = 512;         // DenseParams.pipe bit 9: double-buffered tables
 
 // Step stream (host-built, one u32 word stream per history):
 //   header  live[0:24) | j[24:29), bit 31 clear   live = pending slots after this step's

@@ -433,7 +433,8 @@ def test_gpu_dense_team_planner(plan, monkeypatch):
     assert any(e["valid"] == 0 for e in exp)
 
 
-@pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "15", "27", "47", "79", "143", "207"])
+@pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "15", "27", "47", "79", "143", "207",
+                                  "515", "539", "591", "719", "975"])
 def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     """LC_PIPE bit 0 / bit 1: BLOCK / WAVE teams overlap consecutive RETURN steps (step t+1's
     layer q beside step t's layer q + 2, returns read through the previous step's slot, fresh
@@ -441,7 +442,8 @@ def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     failing step is found from the next step's empty frontier). 11 adds barrier-free tile teams
     (the default), 27 also MID teams (widths 12..14 on 256-thread workgroups); 79 WAVE
     histories on the big kernel's waves, 143/207 MID histories as 4-wave teams inside big
-    workgroups (LDS barriers of their own)."""
+    workgroups (LDS barriers of their own). +512: double-buffered tables (a step after an
+    in-word return starts one super-layer after its predecessor)."""
     monkeypatch.setenv("LC_PIPE", pipe)
     hs = [synth.gen_register_keys(24, 600, 5, 0.01, config_id=3, invalid_keys=(1, 7, 16))]
     hs += [synth.gen_register(120, 5, 0.1, 33000 + t, invalid=(t % 2 == 1)) for t in range(8)]
@@ -493,7 +495,7 @@ def _low_slot_rounds(n_rounds, seed, perturb=False):
     return H.encode(ops)
 
 
-@pytest.mark.parametrize("pipe", ["0", "11", "207"])
+@pytest.mark.parametrize("pipe", ["0", "11", "207", "719", "975"])
 def test_gpu_dense_low_slot_orderings(pipe, monkeypatch):
     """The in-word closure's op sequence (0 1 2 0 1 0 2 for three live low ops, a b a for two):
     RETURNs of slot 3 with slots 0..2 pending, writes among them; bit-exact with the oracle,
@@ -578,7 +580,8 @@ def test_gpu_dense_tile_teams_small_tiles(lbits, monkeypatch):
     p.close()
 
 
-@pytest.mark.parametrize("pipe", ["207", "463"], ids=["tokens", "tagged"])
+@pytest.mark.parametrize("pipe", ["207", "463", "719", "975"],
+                         ids=["tokens", "tagged", "tokens-dbl", "tagged-dbl"])
 @pytest.mark.parametrize("rot,lbits", [("1", "14"), ("3", "13"), ("9", "15"), ("9", None)])
 def test_gpu_dense_tile_teams_rotated(rot, lbits, pipe, monkeypatch):
     """LC_TEAM_ROT: a tile team's lowest slots relabelled as its team bits (every tile holds a
