@@ -93,12 +93,17 @@ __device__ __forceinline__ uint32_t block_slot(uint32_t* s_counter, bool pred) {
   return base + (uint32_t)__popcll(below);
 }
 
-// insert key (< 2^48) into an epoch-tagged open-addressing set; 1 = new, 0 = present
+// insert key (< 2^48) into an epoch-tagged open-addressing set; 1 = new, 0 = present. A probe
+// run longer than PROBE_MAX (tables are sized at most half full, where linear probing's runs
+// are a few dozen words) raises PF_OVERFLOW: an over-full table is reported at once instead of
+// every insert scanning the whole table.
+constexpr uint64_t PROBE_MAX = 4096;
 __device__ __forceinline__ int set_insert(uint64_t* T, uint64_t tmask, uint64_t key, uint64_t ep,
                                           unsigned long long* flags) {
   const uint64_t v = (ep << KEY_BITS) | key;
   uint64_t i = mix64(key) & tmask;
-  for (uint64_t probe = 0; probe <= tmask; ++probe) {
+  const uint64_t pmax = tmask < PROBE_MAX ? tmask : PROBE_MAX;
+  for (uint64_t probe = 0; probe <= pmax; ++probe) {
     uint64_t cur = ld_agent(&T[i]);
     if (cur == v) return 0;
     if ((cur >> KEY_BITS) != ep) {  // free in this epoch: claim it
@@ -401,6 +406,10 @@ __global__ void __launch_bounds__(PL) part_step_kernel(StepArgs a, RunArgs r) {
   unsigned long long* out_count = &ctl->oc[r.sp];
   const int tid = threadIdx.x, lane = __lane_id();
   const bool lead = blockIdx.x == 0 && tid == 0;
+  // an earlier step of the chunk overflowed (or aborted): the host starts over or reports
+  // LC_H_CAPACITY after the chunk, so the rest of it does no work (the flags were set by
+  // earlier launches: every workgroup reads the same value)
+  if (ld_agent(&ctl->flags) & (PF_OVERFLOW | PF_STAGE | PF_ABORT)) return;
   // level 0: expand the frontier into stage 0
   if (lead) st_agent(out_count, 0ull);
   const uint64_t nf = ld_agent(&ctl->oc[r.sp ^ 1]);
@@ -485,6 +494,283 @@ __global__ void __launch_bounds__(PL) part_step_kernel(StepArgs a, RunArgs r) {
   if (lane == 0 && listed) atomicAdd(&ctl->listed, listed);
 }
 
+// ---- lc_part_run, flow form (world 1, the default): no BFS levels. A step's closure is a
+// set (explored = |S|, the OUT set), so the order its configs are found in does not matter:
+// the level barrier (every candidate of level l absorbed before level l + 1 is expanded) is
+// not needed. A step is one work queue instead. Its items are configs to expand: the frontier
+// F (indices [0, nf)) and every new config of the closure that does not hold the returning
+// op (indices nf + i: Q[i], written with the step's epoch tag above the key, so a consumer
+// polls the word itself). Workgroups claim FL items at a time (one atomic per claim), expand
+// them (FB candidates per thread per batch: every probe load, then every CAS, in flight
+// together), and push the new items with one reservation per wave. The step ends when the
+// items completed equal the items produced (read tail, done, tail again: a completion is
+// counted only after its children's reservations returned), then ONE grid barrier. One
+// cooperative launch runs a chunk of steps; the host reads the per-step OUT counts once per
+// chunk. Same verdict, failing step and explored count as the level kernel and the oracle.
+constexpr int FL = 512;  // threads per workgroup = items per claim
+constexpr int FB = 8;    // candidates per thread per insert batch
+constexpr uint64_t KEY_MASK = (1ull << KEY_BITS) - 1;
+
+// one step's queue counters, each on its own 128-B line (three sets rotate over the steps:
+// step t works on sets[t % 3], reads |F| from sets[(t + 2) % 3].outc, resets sets[(t + 1) % 3])
+struct FlowSet {
+  unsigned long long head, pad0[15];
+  unsigned long long tail, pad1[15];
+  unsigned long long done, pad2[15];
+  unsigned long long outc, pad3[15];
+};
+
+struct FlowArgs {
+  uint64_t* S;
+  uint64_t* O;
+  uint64_t tmask;
+  uint64_t* L[2];  // frontier / OUT lists: step t reads L[t & 1], writes L[(t + 1) & 1]
+  uint64_t list_cap;
+  uint64_t* Q;
+  uint64_t qcap;
+  const StepArgs* steps;  // [t1 - t0]; StepArgs.pad = the step's set epoch
+  FlowSet* sets;
+  PartCtl* ctl;
+  PartBar* bar;
+  unsigned long long* flog;  // OUT count per step of the chunk
+  int64_t t0, t1;
+  uint32_t nwg;
+  int32_t mask_bits;
+};
+
+__device__ __forceinline__ bool grid_sync(PartBar* bar, uint32_t nwg, PartCtl* ctl, int* s_abort) {
+  RunArgs r{};
+  r.bar = bar;
+  r.nwg = nwg;
+  r.ctl = ctl;
+  return run_sync(r, s_abort);
+}
+
+// Insert FB keys (has[u]) into set T at once: every probe load, then every CAS, in flight
+// together; a collision (another key of this epoch in the home word, or a lost race) falls
+// back to set_insert's probe run. isnew[u] = 1 for a key this call added.
+__device__ __forceinline__ void insert_batch(uint64_t* T, uint64_t tmask, const uint64_t* key, const bool* has,
+                                             uint64_t ep, unsigned long long* flags, bool* isnew) {
+  uint64_t cur[FB], pos[FB];
+#pragma unroll
+  for (int u = 0; u < FB; ++u) {
+    pos[u] = mix64(key[u]) & tmask;
+    cur[u] = has[u] ? ld_agent(&T[pos[u]]) : 0ull;
+  }
+  uint64_t old[FB];
+  bool tried[FB];
+#pragma unroll
+  for (int u = 0; u < FB; ++u) {
+    const uint64_t v = (ep << KEY_BITS) | key[u];
+    tried[u] = has[u] && cur[u] != v && (cur[u] >> KEY_BITS) != ep;
+    old[u] = tried[u] ? atomicCAS((unsigned long long*)&T[pos[u]], (unsigned long long)cur[u],
+                                  (unsigned long long)v)
+                      : 0ull;
+  }
+#pragma unroll
+  for (int u = 0; u < FB; ++u) {
+    const uint64_t v = (ep << KEY_BITS) | key[u];
+    isnew[u] = false;
+    if (!has[u] || cur[u] == v) continue;
+    if (tried[u] && old[u] == cur[u]) isnew[u] = true;
+    else if (!(tried[u] && old[u] == v)) isnew[u] = set_insert(T, tmask, key[u], ep, flags) != 0;
+  }
+}
+
+// Wave-aggregated append of each lane's n items (vals[0..n)) at *counter: one atomic per wave.
+// Returns false where an item fell beyond cap (the caller raised PF_OVERFLOW).
+template <int N>
+__device__ __forceinline__ bool wave_append(unsigned long long* counter, uint64_t* dst, uint64_t cap,
+                                            const uint64_t* vals, const bool* keep, uint64_t tag) {
+  uint32_t n = 0;
+#pragma unroll
+  for (int u = 0; u < N; ++u) n += keep[u];
+  const int lane = __lane_id();
+  uint32_t x = n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  const uint32_t tot = __shfl(x, 63, 64);
+  if (tot == 0) return true;
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(counter, (unsigned long long)tot);
+  base = __shfl(base, 0, 64);
+  uint64_t pos = base + (x - n);
+  bool ok = true;
+#pragma unroll
+  for (int u = 0; u < N; ++u)
+    if (keep[u]) {
+      if (pos < cap) st_agent(&dst[pos], vals[u] | tag);
+      else ok = false;
+      ++pos;
+    }
+  return ok;
+}
+
+__global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
+  __shared__ uint64_t s_ops[PS_MAX];
+  __shared__ unsigned long long s_c0, s_total;
+  __shared__ int s_abort, s_state;
+  PartCtl* const ctl = r.ctl;
+  // an earlier chunk overflowed or aborted: nothing more to do (set by earlier launches)
+  if (ld_agent(&ctl->flags) & (PF_OVERFLOW | PF_STAGE | PF_ABORT)) return;
+  const int tid = threadIdx.x;
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  const uint64_t mmask = (1ull << r.mask_bits) - 1;
+  unsigned long long expl = 0, listed = 0, cand = 0;
+  for (int64_t t = r.t0; t < r.t1; ++t) {
+    const StepArgs& a = r.steps[t - r.t0];
+    FlowSet* const cs = &r.sets[t % 3];
+    FlowSet* const ps = &r.sets[(t + 2) % 3];
+    const uint64_t nf = ld_agent(&ps->outc);
+    if (nf == 0 && t > 0) break;  // step t - 1 returned an empty frontier (every workgroup sees it)
+    if (lead) {  // the next step's counters (last used by step t - 2, read by step t - 1 at its start)
+      FlowSet* const nx = &r.sets[(t + 1) % 3];
+      st_agent(&nx->head, 0ull);
+      st_agent(&nx->tail, 0ull);
+      st_agent(&nx->done, 0ull);
+      st_agent(&nx->outc, 0ull);
+    }
+    if (tid < PS_MAX) s_ops[tid] = a.ops[tid];
+    const uint64_t live = a.live, bitj = a.bitj;
+    const uint64_t ep = (uint64_t)(uint32_t)a.pad;
+    const uint64_t tag = ep << KEY_BITS;
+    const int wd = live ? 64 - __builtin_clzll(live) : 0;
+    const uint64_t* const F = r.L[t & 1];
+    uint64_t* const OUT = r.L[(t + 1) & 1];
+    __syncthreads();
+    bool fin = false;
+    while (!fin) {
+      if (tid == 0) s_c0 = atomicAdd(&cs->head, (unsigned long long)FL);
+      __syncthreads();
+      const uint64_t idx = s_c0 + (uint64_t)tid;
+      bool pend = true;
+      const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+      for (long spin = 0;; ++spin) {
+        if (tid == 0) s_total = nf + ld_agent(&cs->tail);
+        __syncthreads();
+        const bool ready = pend && idx < s_total;
+        uint64_t c = 0;
+        bool item = false;  // a config to expand or return
+        if (ready) {
+          pend = false;
+          if (idx < nf) {  // written in this launch by the previous step: read past the caches
+            c = ld_agent(&F[idx]), item = true;
+          } else if (idx - nf < r.qcap) {
+            const uint64_t* q = &r.Q[idx - nf];
+            uint64_t wv = ld_agent(q);
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (long k = 1; (wv & ~KEY_MASK) != tag; ++k) {  // reserved, not yet written
+              __builtin_amdgcn_s_sleep(1);
+              wv = ld_agent(q);
+              if ((k & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+                atomicOr(&ctl->flags, (unsigned long long)PF_ABORT);
+                break;
+              }
+            }
+            c = wv & KEY_MASK, item = (wv & ~KEY_MASK) == tag;
+          }  // else: beyond the queue (PF_OVERFLOW was raised by its producer): dropped
+        }
+        listed += item;
+        // a config holding the returning op (frontier only): its image goes to OUT
+        bool dret[1] = {item && (c & bitj) != 0};
+        uint64_t dkey[1] = {c & ~bitj};
+        bool dnew[1] = {false};
+        if (__any(dret[0])) {
+          bool hs[FB];
+          uint64_t ks[FB];
+          bool nw[FB];
+#pragma unroll
+          for (int u = 0; u < FB; ++u) hs[u] = u == 0 && dret[0], ks[u] = u == 0 ? dkey[0] : 0ull;
+          insert_batch(r.O, r.tmask, ks, hs, ep, &ctl->flags, nw);
+          dnew[0] = nw[0];
+        }
+        if (!wave_append<1>(&cs->outc, OUT, r.list_cap, dkey, dnew, 0ull))
+          atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+        // expand: each pending op not in c's mask, FB candidates at a time
+        const bool expand = item && !(c & bitj);
+        const int64_t st = (int64_t)(c >> r.mask_bits);
+        for (int k0 = 0; k0 < wd; k0 += FB) {
+          uint64_t ks[FB];
+          bool hs[FB], nw[FB];
+#pragma unroll
+          for (int u = 0; u < FB; ++u) {
+            const int k = k0 + u;
+            hs[u] = false;
+            ks[u] = 0;
+            if (expand && k < wd && ((live >> k) & 1) && !((c >> k) & 1)) {
+              const uint64_t op = s_ops[k];
+              const int32_t ea = (int32_t)(uint32_t)op, nb = (int32_t)(uint32_t)(op >> 32);
+              if (ea == -1 || ea == st) {
+                const uint64_t ns = nb < 0 ? (uint64_t)st : (uint64_t)nb;
+                ks[u] = (ns << r.mask_bits) | (c & mmask) | (1ull << k);
+                hs[u] = true;
+              }
+            }
+            cand += hs[u];
+          }
+          if (!__any(hs[0] | hs[1] | hs[2] | hs[3] | hs[4] | hs[5] | hs[6] | hs[7])) continue;
+          insert_batch(r.S, r.tmask, ks, hs, ep, &ctl->flags, nw);
+          bool toq[FB], too[FB];
+          uint64_t ok[FB];
+#pragma unroll
+          for (int u = 0; u < FB; ++u) {
+            expl += nw[u];
+            toq[u] = nw[u] && !(ks[u] & bitj);
+            too[u] = nw[u] && (ks[u] & bitj);
+            ok[u] = ks[u] & ~bitj;
+          }
+          // new configs holding j (linearized the returning op): their images to OUT
+          if (__any(too[0] | too[1] | too[2] | too[3] | too[4] | too[5] | too[6] | too[7])) {
+            bool on[FB];
+            insert_batch(r.O, r.tmask, ok, too, ep, &ctl->flags, on);
+            if (!wave_append<FB>(&cs->outc, OUT, r.list_cap, ok, on, 0ull))
+              atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+          }
+          // the others are new items of this step
+          if (!wave_append<FB>(&cs->tail, r.Q, r.qcap, ks, toq, tag))
+            atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+        }
+        // completions of this pass, counted after their children's reservations returned
+        const int ndone = __syncthreads_count(ready);
+        if (tid == 0 && ndone) atomicAdd(&cs->done, (unsigned long long)ndone);
+        if (__syncthreads_count(pend) == 0) break;  // the whole claim is done: claim more
+        if (tid == 0) {  // the step is finished when every item produced is completed
+          const unsigned long long t1 = ld_agent(&cs->tail), d = ld_agent(&cs->done), t2 = ld_agent(&cs->tail);
+          s_state = (t1 == t2 && d == nf + t1) ? 1 : 0;
+          if (!s_state) {
+            __builtin_amdgcn_s_sleep(2);
+            if ((spin & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t_start > 2000000000ull ||
+                                      (ld_agent(&ctl->flags) & PF_ABORT))) {
+              atomicOr(&ctl->flags, (unsigned long long)PF_ABORT);
+              s_state = 2;
+            }
+          }
+        }
+        __syncthreads();
+        if (s_state) {
+          fin = true;
+          break;
+        }
+      }
+    }
+    if (!grid_sync(r.bar, r.nwg, ctl, &s_abort)) return;
+    if (lead) r.flog[t - r.t0] = ld_agent(&cs->outc);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    expl += __shfl_down(expl, off, 64);
+    listed += __shfl_down(listed, off, 64);
+    cand += __shfl_down(cand, off, 64);
+  }
+  if (__lane_id() == 0) {
+    if (expl) atomicAdd(&ctl->explored, expl);
+    if (listed) atomicAdd(&ctl->listed, listed);
+    if (cand) atomicAdd(&ctl->cand, cand);
+  }
+}
+
 void set_msg(char* err, int32_t len, const char* fmt, ...) {
   if (!err || len <= 0) return;
   va_list ap;
@@ -527,6 +813,12 @@ struct lc_part {
   unsigned long long* hflog = nullptr;
   int run_grid = 0;
   uint64_t run_cap = 0;       // entries of stage and stage2 as lc_part_run sized them
+  // lc_part_run, flow form: queue counters, item queue, per-chunk step arguments
+  FlowSet* fsets = nullptr;
+  uint64_t* Q = nullptr;
+  StepArgs* dsteps = nullptr;
+  StepArgs* hsteps = nullptr;
+  int flow_grid = 0;
   // measurement: HIP events around each kernel (on the caller's stream), algorithmic bytes
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool absorb_pending = false;
@@ -544,8 +836,9 @@ struct lc_part {
 
   ~lc_part() {
     for (void* q : {(void*)S, (void*)O, (void*)F, (void*)OUTL, (void*)Lb[0], (void*)Lb[1], (void*)stage,
-                    (void*)ctl, (void*)stage2, (void*)bar, (void*)flog})
+                    (void*)ctl, (void*)stage2, (void*)bar, (void*)flog, (void*)fsets, (void*)Q, (void*)dsteps})
       if (q) (void)hipFree(q);
+    if (hsteps) (void)hipHostFree(hsteps);
     if (hctl) (void)hipHostFree(hctl);
     if (hflog) (void)hipHostFree(hflog);
     for (hipEvent_t e : ev)
@@ -590,12 +883,118 @@ int part_begin(lc_part* p, int64_t t, hipStream_t s, char* err, int32_t err_len)
   p->args.world = p->world;
   p->args.rank = p->rank;
   p->wd = (uint32_t)(64 - __builtin_clzll(p->live));
-  if (++p->epoch > EPOCH_MAX) {  // epochs wrapped: clear both sets once
+  if (++p->epoch > EPOCH_MAX) {  // epochs wrapped: clear both sets (and the flow queue) once
     PT_TRY(hipMemsetAsync(p->S, 0, sizeof(uint64_t) << p->slog, s));
     PT_TRY(hipMemsetAsync(p->O, 0, sizeof(uint64_t) << p->slog, s));
+    if (p->Q) PT_TRY(hipMemsetAsync(p->Q, 0, sizeof(uint64_t) * p->list_cap, s));
     p->epoch = 1;
   }
   p->t = t;
+  return 0;
+}
+
+// lc_part_run's flow form (part_flow_kernel): one cooperative launch per chunk of steps
+int part_run_flow(lc_part* p, hipStream_t s, int64_t ns, int64_t* out4, char* err, int32_t err_len) {
+  constexpr int64_t CHUNK = 2048;
+  if (!p->fsets) {
+    int occ = 0;
+    PT_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, part_flow_kernel, FL, 0));
+    hipDeviceProp_t prop;
+    PT_TRY(hipGetDeviceProperties(&prop, p->device));
+    if (occ < 1) {
+      set_msg(err, err_len, "part_flow_kernel does not fit a CU");
+      return LC_E_DEVICE;
+    }
+    p->flow_grid = prop.multiProcessorCount;  // one workgroup per CU: co-resident
+    if (const char* e = getenv("LC_PART_GRID"))
+      if (atoi(e) >= 1 && atoi(e) < p->flow_grid) p->flow_grid = atoi(e);
+    if (!p->bar) {
+      PT_TRY(hipMalloc(&p->bar, sizeof(PartBar)));
+      PT_TRY(hipMemset(p->bar, 0, sizeof(PartBar)));
+    }
+    if (!p->flog) {
+      PT_TRY(hipMalloc(&p->flog, CHUNK * sizeof(unsigned long long)));
+      PT_TRY(hipHostMalloc(&p->hflog, CHUNK * sizeof(unsigned long long), hipHostMallocDefault));
+    }
+    PT_TRY(hipMalloc(&p->fsets, 3 * sizeof(FlowSet)));
+    PT_TRY(hipMalloc(&p->Q, sizeof(uint64_t) * p->list_cap));
+    PT_TRY(hipMemset(p->Q, 0, sizeof(uint64_t) * p->list_cap));
+    PT_TRY(hipMalloc(&p->dsteps, CHUNK * sizeof(StepArgs)));
+    PT_TRY(hipHostMalloc(&p->hsteps, CHUNK * sizeof(StepArgs), hipHostMallocDefault));
+  }
+  // step 0 reads |F| = 1 (the initial config, key 0, in p->F) from sets[2]
+  PT_TRY(hipMemsetAsync(p->fsets, 0, 3 * sizeof(FlowSet), s));
+  const unsigned long long one = 1;
+  PT_TRY(hipMemcpyAsync(&p->fsets[2].outc, &one, sizeof one, hipMemcpyHostToDevice, s));
+  uint64_t* const L0 = p->F;
+  uint64_t* const L1 = p->OUTL;
+  PT_TRY(hipEventRecord(p->ev[0], s));
+  int64_t t = 0, fail = -1;
+  uint64_t flags = 0;
+  while (t < ns && fail < 0) {
+    const int64_t c0 = t, c1 = std::min(ns, t + CHUNK);
+    for (int64_t u = c0; u < c1; ++u) {
+      int rc = part_begin(p, u, s, err, err_len);
+      if (rc) return rc;
+      p->hsteps[u - c0] = p->args;
+      p->hsteps[u - c0].pad = (int32_t)p->epoch;
+      p->live &= ~p->args.bitj;
+    }
+    PT_TRY(hipMemcpyAsync(p->dsteps, p->hsteps, sizeof(StepArgs) * (size_t)(c1 - c0), hipMemcpyHostToDevice, s));
+    FlowArgs fa{};
+    fa.S = p->S;
+    fa.O = p->O;
+    fa.tmask = (1ull << p->slog) - 1;
+    fa.L[0] = L0;
+    fa.L[1] = L1;
+    fa.list_cap = p->list_cap;
+    fa.Q = p->Q;
+    fa.qcap = p->list_cap;
+    fa.steps = p->dsteps;
+    fa.sets = p->fsets;
+    fa.ctl = p->ctl;
+    fa.bar = p->bar;
+    fa.flog = p->flog;
+    fa.t0 = c0;
+    fa.t1 = c1;
+    fa.nwg = (uint32_t)p->flow_grid;
+    fa.mask_bits = p->mask_bits;
+    void* kargs[] = {(void*)&fa};
+    PT_TRY(hipLaunchCooperativeKernel((const void*)part_flow_kernel, dim3(p->flow_grid), dim3(FL), kargs, 0, s));
+    PT_TRY(hipMemcpyAsync(p->hflog, p->flog, sizeof(unsigned long long) * (size_t)(c1 - c0), hipMemcpyDeviceToHost,
+                          s));
+    int rc = part_read_ctl(p, s, err, err_len);
+    if (rc) return rc;
+    flags = p->hctl->flags;
+    t = c1;
+    if (flags) break;
+    for (int64_t i = 0; i < c1 - c0; ++i)
+      if (p->hflog[i] == 0) {
+        fail = c0 + i;
+        break;
+      }
+  }
+  PT_TRY(hipEventRecord(p->ev[1], s));
+  int rc = part_read_ctl(p, s, err, err_len);
+  if (rc) return rc;
+  flags = p->hctl->flags;
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, p->ev[0], p->ev[1]) == hipSuccess) p->kernel_ms += ms;
+  if (flags & PF_ABORT) {
+    set_msg(err, err_len, "part_flow_kernel: watchdog expired");
+    return LC_E_DEVICE;
+  }
+  if (flags & (PF_OVERFLOW | PF_STAGE)) {
+    set_msg(err, err_len, "frontier exceeded the partition capacity (LC_H_CAPACITY)");
+    return LC_H_CAPACITY;
+  }
+  // read each item (8 B), probe + CAS each candidate (16 B), write each new
+  // config (8 B, at most one per candidate)
+  p->alg_bytes += 8.0 * (double)p->hctl->listed + 24.0 * (double)p->hctl->cand;
+  out4[0] = fail >= 0 ? fail + 1 : t;
+  out4[1] = fail;
+  out4[2] = 0;  // no BFS levels in the flow form
+  out4[3] = (int64_t)p->hctl->explored;
   return 0;
 }
 
@@ -861,6 +1260,9 @@ int32_t lc_part_run(lc_part* p, void* stream, int64_t max_steps, int64_t* out4, 
   }
   hipStream_t s = (hipStream_t)stream;
   PT_TRY(hipSetDevice(p->device));
+  const int64_t ns_flow = max_steps >= 0 ? std::min<int64_t>(p->enc.n_steps(0), max_steps) : p->enc.n_steps(0);
+  const char* fe = getenv("LC_PART_FLOW");  // 0: the level kernel (part_step_kernel)
+  if (!fe || atoi(fe) != 0) return part_run_flow(p, s, ns_flow, out4, err, err_len);
   constexpr int64_t CHUNK = 2048;
   if (!p->bar) {
     PT_TRY(hipMalloc(&p->bar, sizeof(PartBar)));

@@ -133,8 +133,10 @@ def test_gpu_c4_full_size_dense():
     assert int(g["explored"][0]) == C4_EXPLORED
 
 
-def test_gpu_c4_full_size_partitioned_world1():
+@pytest.mark.parametrize("flow", ["1", "0"], ids=["flow", "levels"])
+def test_gpu_c4_full_size_partitioned_world1(flow, monkeypatch):
     from lincheck import partition
+    monkeypatch.setenv("LC_PART_FLOW", flow)
     h = synth.gen_config("c4")
     r = partition.check_partitioned(h, capacity_log2=25)
     assert (r["valid"], r["err"], r["explored"]) == (1, 0, C4_EXPLORED)
@@ -719,37 +721,49 @@ def _part_cases():
     return hs
 
 
-@pytest.mark.parametrize("device_loop", [True, False], ids=["lc_part_run", "level_protocol"])
-def test_gpu_partitioned_world1_vs_oracle(device_loop):
+@pytest.mark.parametrize("device_loop,flow", [(True, "1"), (True, "0"), (False, "1")],
+                         ids=["lc_part_run_flow", "lc_part_run_levels", "level_protocol"])
+def test_gpu_partitioned_world1_vs_oracle(device_loop, flow, monkeypatch):
+    """World 1: lc_part_run's flow form (one work queue per step, no level barriers: the
+    default), its level kernel (LC_PART_FLOW=0) and the host-driven level protocol."""
     from lincheck import partition
+    monkeypatch.setenv("LC_PART_FLOW", flow)
     for i, h in enumerate(_part_cases()):
         r = partition.check_partitioned(h, device_loop=device_loop)
         assert _part_row(r) == _oracle_part_row(h), (i, r)
 
 
-def test_gpu_partitioned_matches_dense_on_c2_slice():
+def test_gpu_partitioned_matches_dense_on_c2_slice(monkeypatch):
     from lincheck import partition
     h = synth.gen_config("c2", scale=0.3)
-    r = partition.check_partitioned(h)
+    r = partition.check_partitioned(h)  # flow form
     q = partition.check_partitioned(h, device_loop=False)
+    monkeypatch.setenv("LC_PART_FLOW", "0")
+    lv = partition.check_partitioned(h)  # level kernel
     g = _lib.check(1, 0, h)
     assert (r["valid"], r["explored"]) == (int(g["valid"][0]), int(g["explored"][0]))
-    assert (q["valid"], q["explored"], q["levels"]) == (r["valid"], r["explored"], r["levels"])
+    assert (q["valid"], q["explored"]) == (r["valid"], r["explored"])
+    assert (q["valid"], q["explored"], q["levels"]) == (lv["valid"], lv["explored"], lv["levels"])
 
 
-@pytest.mark.parametrize("device_loop", [True, False], ids=["lc_part_run", "level_protocol"])
-def test_gpu_partitioned_capacity_is_unknown(device_loop):
+@pytest.mark.parametrize("device_loop,flow", [(True, "1"), (True, "0"), (False, "1")],
+                         ids=["lc_part_run_flow", "lc_part_run_levels", "level_protocol"])
+def test_gpu_partitioned_capacity_is_unknown(device_loop, flow, monkeypatch):
     from lincheck import partition
+    monkeypatch.setenv("LC_PART_FLOW", flow)
     h = synth.gen_config("c2", scale=0.1)
     r = partition.check_partitioned(h, capacity_log2=10, device_loop=device_loop)
     assert r["valid"] == 2 and r["err"] == -7
 
 
-def test_gpu_partitioned_run_stage_retry_and_max_steps():
-    """lc_part_run with lists of 2^11: levels whose candidates outgrow the stage make it start
-    over with a 4x stage (same answer as the oracle when the sets still fit); max_steps stops
-    early with the explored count of the steps run."""
+@pytest.mark.parametrize("flow", ["1", "0"], ids=["flow", "levels"])
+def test_gpu_partitioned_run_stage_retry_and_max_steps(flow, monkeypatch):
+    """lc_part_run with lists of 2^11: levels whose candidates outgrow the stage make the level
+    kernel start over with a 4x stage, a full flow queue reports LC_H_CAPACITY (the oracle's
+    answer whenever the sets still fit); max_steps stops early with the explored count of the
+    steps run."""
     from lincheck import partition
+    monkeypatch.setenv("LC_PART_FLOW", flow)
     for h in _part_cases()[:4]:
         r = partition.check_partitioned(h, capacity_log2=11)
         if r["err"] == 0:
@@ -765,7 +779,8 @@ def test_gpu_partitioned_run_stage_retry_and_max_steps():
         full = partition.search(q, max_steps=40, device_loop=False)
     finally:
         q.close()
-    assert (steps, fail, levels, explored) == (40, -1, full["levels"], full["explored"])
+    assert (steps, fail, explored) == (40, -1, full["explored"])
+    assert levels == (full["levels"] if flow == "0" else 0)
 
 
 def _gpu_part_worker(rank, world, port, q):
