@@ -495,29 +495,35 @@ __global__ void __launch_bounds__(PL) part_step_kernel(StepArgs a, RunArgs r) {
 }
 
 // ---- lc_part_run, flow form (world 1, the default): no BFS levels. A step's closure is a
-// set (explored = |S|, the OUT set), so the order its configs are found in does not matter:
-// the level barrier (every candidate of level l absorbed before level l + 1 is expanded) is
-// not needed. A step is one work queue instead. Its items are configs to expand: the frontier
-// F (indices [0, nf)) and every new config of the closure that does not hold the returning
-// op (indices nf + i: Q[i], written with the step's epoch tag above the key, so a consumer
-// polls the word itself). Workgroups claim FL items at a time (one atomic per claim), expand
-// them (FB candidates per thread per batch: every probe load, then every CAS, in flight
-// together), and push the new items with one reservation per wave. The step ends when the
-// items completed equal the items produced (read tail, done, tail again: a completion is
-// counted only after its children's reservations returned), then ONE grid barrier. One
-// cooperative launch runs a chunk of steps; the host reads the per-step OUT counts once per
-// chunk. Same verdict, failing step and explored count as the level kernel and the oracle.
-constexpr int FL = 512;  // threads per workgroup = items per claim
-constexpr int FB = 8;    // candidates per thread per insert batch
+// set (explored = |S|, the OUT set), so the order its configs are found in does not matter and
+// the level barrier (every candidate of level l absorbed before level l + 1 is expanded) is not
+// needed. Each workgroup works through ITEMS (configs to expand): its share of the frontier F,
+// then the new configs its own passes found (an LDS ring: no global claim, no hand-off
+// latency), then, when both are empty, the global overflow queue Q that children go to when a
+// ring is full (tagged words: [epoch | key], polled by the consumer). A pass takes up to FL
+// items (one per thread) and expands them FB candidates at a time: the S probes and, for
+// candidates holding the returning op j, the O probes of their images are issued together
+// (every j-holding candidate is in S, new or not, so its image belongs to OUT either way), then
+// the CASes together. New OUT configs collect in an LDS buffer flushed once per step. The step
+// ends when R = (children produced) - (items completed), summed over every pass, reaches
+// -|F|: each workgroup adds its pass's net once, in order, after the pass, and a child pushed
+// to Q is counted BEFORE it is published, so R never reaches -|F| while an item is pending.
+// Then ONE grid barrier. One cooperative launch runs a chunk of steps; the host reads the
+// per-step OUT counts once per chunk. Same verdict, failing step and explored count as the
+// level kernel and the oracle.
+constexpr int FL = 512;   // threads per workgroup = items per pass
+constexpr int FB = 10;    // candidates per thread per insert batch
+constexpr int LQ = 4096;  // LDS item ring per workgroup (entries)
+constexpr int LO = 2048;  // LDS OUT buffer per workgroup (entries)
 constexpr uint64_t KEY_MASK = (1ull << KEY_BITS) - 1;
 
-// one step's queue counters, each on its own 128-B line (three sets rotate over the steps:
-// step t works on sets[t % 3], reads |F| from sets[(t + 2) % 3].outc, resets sets[(t + 1) % 3])
+// one step's counters, each on its own 128-B line (three sets rotate over the steps: step t
+// works on sets[t % 3], reads |F| from sets[(t + 2) % 3].outc, resets sets[(t + 1) % 3])
 struct FlowSet {
-  unsigned long long head, pad0[15];
-  unsigned long long tail, pad1[15];
-  unsigned long long done, pad2[15];
-  unsigned long long outc, pad3[15];
+  unsigned long long head, pad0[15];  // overflow queue Q: claimed
+  unsigned long long tail, pad1[15];  //   reserved
+  unsigned long long outc, pad2[15];  // OUT list entries
+  long long R, pad3[15];              // children produced - items completed
 };
 
 struct FlowArgs {
@@ -546,34 +552,71 @@ __device__ __forceinline__ bool grid_sync(PartBar* bar, uint32_t nwg, PartCtl* c
   return run_sync(r, s_abort);
 }
 
-// Insert FB keys (has[u]) into set T at once: every probe load, then every CAS, in flight
-// together; a collision (another key of this epoch in the home word, or a lost race) falls
-// back to set_insert's probe run. isnew[u] = 1 for a key this call added.
-__device__ __forceinline__ void insert_batch(uint64_t* T, uint64_t tmask, const uint64_t* key, const bool* has,
-                                             uint64_t ep, unsigned long long* flags, bool* isnew) {
-  uint64_t cur[FB], pos[FB];
+// Insert N keys (key[u] & ~clr where has[u]) into set T at once: every probe load, then
+// every CAS, in flight together; a collision (another key of this epoch in the home word, or a
+// lost race) falls back to set_insert's probe run. isnew[u] = a key this call added.
+template <int N>
+__device__ __forceinline__ void insert_batch(uint64_t* T, uint64_t tmask, const uint64_t* key, uint64_t clr,
+                                             const bool* has, uint64_t ep, unsigned long long* flags, bool* isnew) {
+  uint64_t cur[N];
 #pragma unroll
-  for (int u = 0; u < FB; ++u) {
-    pos[u] = mix64(key[u]) & tmask;
-    cur[u] = has[u] ? ld_agent(&T[pos[u]]) : 0ull;
-  }
-  uint64_t old[FB];
-  bool tried[FB];
+  for (int u = 0; u < N; ++u) cur[u] = has[u] ? ld_agent(&T[mix64(key[u] & ~clr) & tmask]) : 0ull;
+  uint64_t old[N];
 #pragma unroll
-  for (int u = 0; u < FB; ++u) {
-    const uint64_t v = (ep << KEY_BITS) | key[u];
-    tried[u] = has[u] && cur[u] != v && (cur[u] >> KEY_BITS) != ep;
-    old[u] = tried[u] ? atomicCAS((unsigned long long*)&T[pos[u]], (unsigned long long)cur[u],
-                                  (unsigned long long)v)
-                      : 0ull;
+  for (int u = 0; u < N; ++u) {
+    const uint64_t v = (ep << KEY_BITS) | (key[u] & ~clr);
+    const bool tried = has[u] && cur[u] != v && (cur[u] >> KEY_BITS) != ep;
+    old[u] = tried ? atomicCAS((unsigned long long*)&T[mix64(key[u] & ~clr) & tmask], (unsigned long long)cur[u],
+                               (unsigned long long)v)
+                   : ~cur[u];  // (never equal to cur or v: "not tried")
   }
 #pragma unroll
-  for (int u = 0; u < FB; ++u) {
-    const uint64_t v = (ep << KEY_BITS) | key[u];
+  for (int u = 0; u < N; ++u) {
+    const uint64_t v = (ep << KEY_BITS) | (key[u] & ~clr);
     isnew[u] = false;
     if (!has[u] || cur[u] == v) continue;
-    if (tried[u] && old[u] == cur[u]) isnew[u] = true;
-    else if (!(tried[u] && old[u] == v)) isnew[u] = set_insert(T, tmask, key[u], ep, flags) != 0;
+    if (old[u] == cur[u]) isnew[u] = true;
+    else if (old[u] != v) isnew[u] = set_insert(T, tmask, key[u] & ~clr, ep, flags) != 0;
+  }
+}
+
+// S and O inserts of one batch at once: key[u] into S where has[u], key[u] & ~clr into O where
+// hj[u]; every probe load of both, then every CAS of both, in flight together.
+template <int N>
+__device__ __forceinline__ void insert_batch2(uint64_t* S, uint64_t* O, uint64_t tmask, const uint64_t* key,
+                                              uint64_t clr, const bool* has, const bool* hj, uint64_t ep,
+                                              unsigned long long* flags, bool* snew, bool* onew) {
+  uint64_t cs_[N], co[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    cs_[u] = has[u] ? ld_agent(&S[mix64(key[u]) & tmask]) : 0ull;
+    co[u] = hj[u] ? ld_agent(&O[mix64(key[u] & ~clr) & tmask]) : 0ull;
+  }
+  uint64_t os[N], oo[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const uint64_t vs = (ep << KEY_BITS) | key[u], vo = (ep << KEY_BITS) | (key[u] & ~clr);
+    const bool ts = has[u] && cs_[u] != vs && (cs_[u] >> KEY_BITS) != ep;
+    const bool to = hj[u] && co[u] != vo && (co[u] >> KEY_BITS) != ep;
+    os[u] = ts ? atomicCAS((unsigned long long*)&S[mix64(key[u]) & tmask], (unsigned long long)cs_[u],
+                           (unsigned long long)vs)
+               : ~cs_[u];
+    oo[u] = to ? atomicCAS((unsigned long long*)&O[mix64(key[u] & ~clr) & tmask], (unsigned long long)co[u],
+                           (unsigned long long)vo)
+               : ~co[u];
+  }
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const uint64_t vs = (ep << KEY_BITS) | key[u], vo = (ep << KEY_BITS) | (key[u] & ~clr);
+    snew[u] = onew[u] = false;
+    if (has[u] && cs_[u] != vs) {
+      if (os[u] == cs_[u]) snew[u] = true;
+      else if (os[u] != vs) snew[u] = set_insert(S, tmask, key[u], ep, flags) != 0;
+    }
+    if (hj[u] && co[u] != vo) {
+      if (oo[u] == co[u]) onew[u] = true;
+      else if (oo[u] != vo) onew[u] = set_insert(O, tmask, key[u] & ~clr, ep, flags) != 0;
+    }
   }
 }
 
@@ -581,7 +624,7 @@ __device__ __forceinline__ void insert_batch(uint64_t* T, uint64_t tmask, const 
 // Returns false where an item fell beyond cap (the caller raised PF_OVERFLOW).
 template <int N>
 __device__ __forceinline__ bool wave_append(unsigned long long* counter, uint64_t* dst, uint64_t cap,
-                                            const uint64_t* vals, const bool* keep, uint64_t tag) {
+                                            const uint64_t* vals, uint64_t clr, const bool* keep, uint64_t tag) {
   uint32_t n = 0;
 #pragma unroll
   for (int u = 0; u < N; ++u) n += keep[u];
@@ -602,7 +645,7 @@ __device__ __forceinline__ bool wave_append(unsigned long long* counter, uint64_
 #pragma unroll
   for (int u = 0; u < N; ++u)
     if (keep[u]) {
-      if (pos < cap) st_agent(&dst[pos], vals[u] | tag);
+      if (pos < cap) st_agent(&dst[pos], (vals[u] & ~clr) | tag);
       else ok = false;
       ++pos;
     }
@@ -610,8 +653,11 @@ __device__ __forceinline__ bool wave_append(unsigned long long* counter, uint64_
 }
 
 __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
+  __shared__ uint64_t s_q[LQ];  // item ring
+  __shared__ uint64_t s_o[LO];  // OUT buffer
   __shared__ uint64_t s_ops[PS_MAX];
-  __shared__ unsigned long long s_c0, s_total;
+  __shared__ unsigned s_qh, s_qt, s_push, s_on, s_n, s_src, s_ring;
+  __shared__ unsigned long long s_f, s_fend, s_g0, s_base;
   __shared__ int s_abort, s_state;
   PartCtl* const ctl = r.ctl;
   // an earlier chunk overflowed or aborted: nothing more to do (set by earlier launches)
@@ -630,131 +676,217 @@ __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
       FlowSet* const nx = &r.sets[(t + 1) % 3];
       st_agent(&nx->head, 0ull);
       st_agent(&nx->tail, 0ull);
-      st_agent(&nx->done, 0ull);
       st_agent(&nx->outc, 0ull);
+      st_agent(&nx->R, 0ll);
     }
     if (tid < PS_MAX) s_ops[tid] = a.ops[tid];
+    if (tid == 0) {  // this workgroup's share of F, an empty ring and OUT buffer
+      s_f = nf * blockIdx.x / r.nwg;
+      s_fend = nf * (blockIdx.x + 1) / r.nwg;
+      s_qh = s_qt = 0;
+      s_on = 0;
+    }
     const uint64_t live = a.live, bitj = a.bitj;
     const uint64_t ep = (uint64_t)(uint32_t)a.pad;
     const uint64_t tag = ep << KEY_BITS;
     const int wd = live ? 64 - __builtin_clzll(live) : 0;
     const uint64_t* const F = r.L[t & 1];
     uint64_t* const OUT = r.L[(t + 1) & 1];
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
-    bool fin = false;
-    while (!fin) {
-      if (tid == 0) s_c0 = atomicAdd(&cs->head, (unsigned long long)FL);
-      __syncthreads();
-      const uint64_t idx = s_c0 + (uint64_t)tid;
-      bool pend = true;
-      const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-      for (long spin = 0;; ++spin) {
-        if (tid == 0) s_total = nf + ld_agent(&cs->tail);
-        __syncthreads();
-        const bool ready = pend && idx < s_total;
-        uint64_t c = 0;
-        bool item = false;  // a config to expand or return
-        if (ready) {
-          pend = false;
-          if (idx < nf) {  // written in this launch by the previous step: read past the caches
-            c = ld_agent(&F[idx]), item = true;
-          } else if (idx - nf < r.qcap) {
-            const uint64_t* q = &r.Q[idx - nf];
-            uint64_t wv = ld_agent(q);
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (long k = 1; (wv & ~KEY_MASK) != tag; ++k) {  // reserved, not yet written
-              __builtin_amdgcn_s_sleep(1);
-              wv = ld_agent(q);
-              if ((k & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
-                atomicOr(&ctl->flags, (unsigned long long)PF_ABORT);
+    for (;;) {
+      // ---- take up to FL items: F share, then the ring, then the overflow queue
+      if (tid == 0) {
+        s_state = 0;
+        s_push = 0;
+        s_ring = 0;
+        if (s_f < s_fend) {
+          s_src = 0;
+          s_n = (unsigned)min<uint64_t>(FL, s_fend - s_f);
+        } else if (s_qt != s_qh) {
+          s_src = 1;
+          s_n = min(FL, (int)(s_qt - s_qh));
+        } else {
+          s_src = 2;
+          s_n = 0;
+          for (long k = 0;; ++k) {  // idle: claim from Q, or see the step finished
+            const unsigned long long h = ld_agent(&cs->head), tl = ld_agent(&cs->tail);
+            if (tl > h) {
+              const unsigned m = (unsigned)min<unsigned long long>(FL, tl - h);
+              if (atomicCAS(&cs->head, h, h + m) == h) {
+                s_g0 = h;
+                s_n = m;
                 break;
               }
+              continue;
             }
-            c = wv & KEY_MASK, item = (wv & ~KEY_MASK) == tag;
-          }  // else: beyond the queue (PF_OVERFLOW was raised by its producer): dropped
-        }
-        listed += item;
-        // a config holding the returning op (frontier only): its image goes to OUT
-        bool dret[1] = {item && (c & bitj) != 0};
-        uint64_t dkey[1] = {c & ~bitj};
-        bool dnew[1] = {false};
-        if (__any(dret[0])) {
-          bool hs[FB];
-          uint64_t ks[FB];
-          bool nw[FB];
-#pragma unroll
-          for (int u = 0; u < FB; ++u) hs[u] = u == 0 && dret[0], ks[u] = u == 0 ? dkey[0] : 0ull;
-          insert_batch(r.O, r.tmask, ks, hs, ep, &ctl->flags, nw);
-          dnew[0] = nw[0];
-        }
-        if (!wave_append<1>(&cs->outc, OUT, r.list_cap, dkey, dnew, 0ull))
-          atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
-        // expand: each pending op not in c's mask, FB candidates at a time
-        const bool expand = item && !(c & bitj);
-        const int64_t st = (int64_t)(c >> r.mask_bits);
-        for (int k0 = 0; k0 < wd; k0 += FB) {
-          uint64_t ks[FB];
-          bool hs[FB], nw[FB];
-#pragma unroll
-          for (int u = 0; u < FB; ++u) {
-            const int k = k0 + u;
-            hs[u] = false;
-            ks[u] = 0;
-            if (expand && k < wd && ((live >> k) & 1) && !((c >> k) & 1)) {
-              const uint64_t op = s_ops[k];
-              const int32_t ea = (int32_t)(uint32_t)op, nb = (int32_t)(uint32_t)(op >> 32);
-              if (ea == -1 || ea == st) {
-                const uint64_t ns = nb < 0 ? (uint64_t)st : (uint64_t)nb;
-                ks[u] = (ns << r.mask_bits) | (c & mmask) | (1ull << k);
-                hs[u] = true;
-              }
+            if (ld_agent(&cs->R) == -(long long)nf) {
+              s_state = 1;
+              break;
             }
-            cand += hs[u];
-          }
-          if (!__any(hs[0] | hs[1] | hs[2] | hs[3] | hs[4] | hs[5] | hs[6] | hs[7])) continue;
-          insert_batch(r.S, r.tmask, ks, hs, ep, &ctl->flags, nw);
-          bool toq[FB], too[FB];
-          uint64_t ok[FB];
-#pragma unroll
-          for (int u = 0; u < FB; ++u) {
-            expl += nw[u];
-            toq[u] = nw[u] && !(ks[u] & bitj);
-            too[u] = nw[u] && (ks[u] & bitj);
-            ok[u] = ks[u] & ~bitj;
-          }
-          // new configs holding j (linearized the returning op): their images to OUT
-          if (__any(too[0] | too[1] | too[2] | too[3] | too[4] | too[5] | too[6] | too[7])) {
-            bool on[FB];
-            insert_batch(r.O, r.tmask, ok, too, ep, &ctl->flags, on);
-            if (!wave_append<FB>(&cs->outc, OUT, r.list_cap, ok, on, 0ull))
-              atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
-          }
-          // the others are new items of this step
-          if (!wave_append<FB>(&cs->tail, r.Q, r.qcap, ks, toq, tag))
-            atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
-        }
-        // completions of this pass, counted after their children's reservations returned
-        const int ndone = __syncthreads_count(ready);
-        if (tid == 0 && ndone) atomicAdd(&cs->done, (unsigned long long)ndone);
-        if (__syncthreads_count(pend) == 0) break;  // the whole claim is done: claim more
-        if (tid == 0) {  // the step is finished when every item produced is completed
-          const unsigned long long t1 = ld_agent(&cs->tail), d = ld_agent(&cs->done), t2 = ld_agent(&cs->tail);
-          s_state = (t1 == t2 && d == nf + t1) ? 1 : 0;
-          if (!s_state) {
-            __builtin_amdgcn_s_sleep(2);
-            if ((spin & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t_start > 2000000000ull ||
-                                      (ld_agent(&ctl->flags) & PF_ABORT))) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((k & 255) == 255 && (__builtin_amdgcn_s_memrealtime() - t_start > 2000000000ull ||
+                                     (ld_agent(&ctl->flags) & PF_ABORT))) {
               atomicOr(&ctl->flags, (unsigned long long)PF_ABORT);
               s_state = 2;
+              break;
             }
           }
         }
-        __syncthreads();
-        if (s_state) {
-          fin = true;
-          break;
+      }
+      __syncthreads();
+      if (s_state) break;
+      const unsigned n = s_n, src = s_src;
+      const unsigned qh0 = s_qh, qt0 = s_qt;
+      const unsigned long long f0 = s_f, g0 = s_g0;
+      uint64_t c = 0;
+      bool item = false;
+      if ((unsigned)tid < n) {
+        if (src == 0) {  // written in this launch by the previous step: read past the caches
+          c = ld_agent(&F[f0 + tid]), item = true;
+        } else if (src == 1) {
+          c = s_q[(qh0 + tid) & (LQ - 1)], item = true;
+        } else if (g0 + tid < r.qcap) {
+          const uint64_t* q = &r.Q[g0 + tid];
+          uint64_t wv = ld_agent(q);
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (long k = 1; (wv & ~KEY_MASK) != tag; ++k) {  // reserved, not yet written
+            __builtin_amdgcn_s_sleep(1);
+            wv = ld_agent(q);
+            if ((k & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+              atomicOr(&ctl->flags, (unsigned long long)PF_ABORT);
+              break;
+            }
+          }
+          c = wv & KEY_MASK, item = (wv & ~KEY_MASK) == tag;
+        }  // else: beyond Q (PF_OVERFLOW was raised by its producer): dropped
+      }
+      __syncthreads();  // every thread has its item: the ring slots may be refilled
+      if (tid == 0) {
+        if (src == 0) s_f = f0 + n;
+        else if (src == 1) s_qh = qh0 + n;
+      }
+      // ring slots free for this pass's children (the same value in every thread): children
+      // reserve positions in order, so the ones that fit are a prefix of the reservations
+      const unsigned qfree = (unsigned)LQ - (qt0 - (src == 1 ? qh0 + n : qh0));
+      listed += item;
+      // OUT configs into the LDS buffer (the global list once it is full)
+      auto emit_out = [&](uint64_t k, bool keep) {
+        if (!keep) return;
+        const unsigned i = atomicAdd(&s_on, 1u);
+        if (i < (unsigned)LO) {
+          s_o[i] = k;
+        } else {
+          const unsigned long long q = atomicAdd(&cs->outc, 1ull);
+          if (q < r.list_cap) st_agent(&OUT[q], k);
+          else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+        }
+      };
+      // a config holding the returning op (frontier only): its image goes to OUT
+      {
+        const bool dret[1] = {item && (c & bitj) != 0};
+        bool dnew[1] = {false};
+        if (__any(dret[0])) insert_batch<1>(r.O, r.tmask, &c, bitj, dret, ep, &ctl->flags, dnew);
+        emit_out(c & ~bitj, dnew[0]);
+      }
+      // expand: each pending op not in c's mask, FB candidates at a time
+      const bool expand = item && !(c & bitj);
+      const int64_t st = (int64_t)(c >> r.mask_bits);
+      unsigned ringc = 0;
+      for (int k0 = 0; k0 < wd; k0 += FB) {
+        uint64_t ks[FB];
+        bool hs[FB], hj[FB], nw[FB], on[FB];
+        bool anyh = false;
+#pragma unroll
+        for (int u = 0; u < FB; ++u) {
+          const int k = k0 + u;
+          hs[u] = false;
+          ks[u] = 0;
+          if (expand && k < wd && ((live >> k) & 1) && !((c >> k) & 1)) {
+            const uint64_t op = s_ops[k];
+            const int32_t ea = (int32_t)(uint32_t)op, nb = (int32_t)(uint32_t)(op >> 32);
+            if (ea == -1 || ea == st) {
+              const uint64_t ns = nb < 0 ? (uint64_t)st : (uint64_t)nb;
+              ks[u] = (ns << r.mask_bits) | (c & mmask) | (1ull << k);
+              hs[u] = true;
+            }
+          }
+          hj[u] = hs[u] && (ks[u] & bitj);
+          cand += hs[u];
+          anyh |= hs[u];
+        }
+        if (!__any(anyh)) continue;
+        // S and O together: a j-holding candidate is in S (new or not), so its image is in OUT
+        insert_batch2<FB>(r.S, r.O, r.tmask, ks, bitj, hs, hj, ep, &ctl->flags, nw, on);
+        bool toq[FB];
+        unsigned nc = 0;
+#pragma unroll
+        for (int u = 0; u < FB; ++u) {
+          expl += nw[u];
+          toq[u] = nw[u] && !hj[u];
+          nc += toq[u];
+          emit_out(ks[u] & ~bitj, on[u]);
+        }
+        // new configs without j are this step's next items: the ring, or Q when it is full
+        unsigned base = 0;
+        if (nc) base = atomicAdd(&s_push, nc);
+        const bool fits = base + nc <= qfree;
+        if (nc && fits) {
+          unsigned pos = qt0 + base;
+#pragma unroll
+          for (int u = 0; u < FB; ++u)
+            if (toq[u]) s_q[(pos++) & (LQ - 1)] = ks[u];
+          ringc += nc;
+        }
+        const bool ov = nc && !fits;
+        if (__any(ov)) {  // count them in R first (returned), then reserve and publish
+          const unsigned nl = ov ? nc : 0;
+          unsigned x = nl;
+          const int lane = __lane_id();
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+          }
+          const unsigned tot = __shfl(x, 63, 64);
+          unsigned long long gb = 0;
+          if (lane == 0) {
+            (void)atomicAdd((unsigned long long*)&cs->R, (unsigned long long)tot);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            gb = atomicAdd(&cs->tail, (unsigned long long)tot);
+          }
+          gb = __shfl(gb, 0, 64);
+          uint64_t pos = gb + (x - nl);
+          if (ov)
+#pragma unroll
+            for (int u = 0; u < FB; ++u)
+              if (toq[u]) {
+                if (pos < r.qcap) st_agent(&r.Q[pos], ks[u] | tag);
+                else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
+                ++pos;
+              }
         }
       }
+      // the pass's net: ring children - items completed, once, after the pass (by one lane:
+      // a ring child's +1 and its later -1 are that lane's atomics on one word, in order)
+      unsigned rs = ringc;
+      for (int off = 32; off > 0; off >>= 1) rs += __shfl_down(rs, off, 64);
+      if (__lane_id() == 0 && rs) atomicAdd(&s_ring, rs);
+      __syncthreads();
+      if (tid == 0) {
+        s_qt = qt0 + s_ring;
+        atomicAdd((unsigned long long*)&cs->R, (unsigned long long)((long long)s_ring - (long long)n));
+      }
+      __syncthreads();
+    }
+    // flush the OUT buffer, then the step's grid barrier
+    const unsigned no = min(s_on, (unsigned)LO);
+    if (tid == 0 && no) s_base = atomicAdd(&cs->outc, (unsigned long long)no);
+    __syncthreads();
+    for (unsigned i = tid; i < no; i += FL) {
+      const unsigned long long q = s_base + i;
+      if (q < r.list_cap) st_agent(&OUT[q], s_o[i]);
+      else atomicOr(&ctl->flags, (unsigned long long)PF_OVERFLOW);
     }
     if (!grid_sync(r.bar, r.nwg, ctl, &s_abort)) return;
     if (lead) r.flog[t - r.t0] = ld_agent(&cs->outc);
