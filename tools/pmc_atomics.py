@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def main(tag, pmc_csv, trace_csv, *kernels):
-    kernels = kernels or ("part_step_kernel", "part_absorb", "part_expand")
+    kernels = kernels or ("part_flow_kernel", "part_step_kernel", "part_absorb", "part_expand")
     cnt = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
     with open(pmc_csv) as fh:

@@ -20,7 +20,10 @@ timeout -s KILL 300 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TCP_TCC_AT
 timeout -k 10 400 $B --workload c4 --partition --steps 1 --warmup 0 > $out/c4_partition_bench.json 2> $out/c4_partition_bench.err || exit 1
 timeout -k 10 400 $B --workload c2 --partition --steps 2 --warmup 1 > $out/c2_partition_bench.json 2> $out/c2_partition_bench.err || exit 1
 timeout -k 10 200 $B --workload c4 --steps 1 --warmup 1 --no-cpu > $out/c4_bench.json 2> $out/c4_bench.err || exit 1
-# device-resident loop (lc_part_run): the atomic counters (the trace ran in profile_round.sh)
+# device-resident loop (lc_part_run, flow kernel by default): kernel trace, then the atomic
+# counters (both may end in rocprofv3's exit-handler crash after the files are written)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/part_trace -o run -- $PP \
+  > $out/part_trace.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc TCC_ATOMIC_sum TCC_EA0_ATOMIC_sum TCP_TCC_ATOMIC_WITH_RET_REQ_sum \
   TCP_TCC_ATOMIC_WITHOUT_RET_REQ_sum --output-format csv -d $out/part_pmc_atomic -o run -- $PP > $out/part_pmc.log 2>&1
 echo done
