@@ -412,7 +412,7 @@ __global__ void __launch_bounds__(PL) part_step_kernel(StepArgs a, RunArgs r) {
   if (ld_agent(&ctl->flags) & (PF_OVERFLOW | PF_STAGE | PF_ABORT)) return;
   // level 0: expand the frontier into stage 0
   if (lead) st_agent(out_count, 0ull);
-  const uint64_t nf = ld_agent(&ctl->oc[r.sp ^ 1]);
+  const uint64_t nf = min<uint64_t>(ld_agent(&ctl->oc[r.sp ^ 1]), r.list_cap);  // (overflowed counts: never beyond the list)
   const uint64_t stride = (uint64_t)r.nwg * PL;
   for (uint64_t it = (uint64_t)blockIdx.x * PL; it < nf; it += stride) {  // block-uniform trip count
     const uint64_t i = it + tid;
@@ -511,8 +511,14 @@ __global__ void __launch_bounds__(PL) part_step_kernel(StepArgs a, RunArgs r) {
 // Then ONE grid barrier. One cooperative launch runs a chunk of steps; the host reads the
 // per-step OUT counts once per chunk. Same verdict, failing step and explored count as the
 // level kernel and the oracle.
-constexpr int FL = 512;   // threads per workgroup = items per pass
-constexpr int FB = 10;    // candidates per thread per insert batch
+constexpr int FL = 512;   // threads per workgroup
+constexpr int FB = 8;     // candidates per thread per insert batch
+// threads per item, per pass: 3 when few items are at hand (thread h of an item takes its
+// candidate batches h, h + 3, ...: one batch each up to 24 pending ops, so the pass is one
+// round of probes and one of CASes), 1 when a pass can fill every thread with an item
+__device__ __forceinline__ unsigned flow_ft(unsigned long long avail) {
+  return avail > 2 * (FL / 3) ? 1u : avail > FL / 3 ? 2u : 3u;
+}
 constexpr int LQ = 4096;  // LDS item ring per workgroup (entries)
 constexpr int LO = 2048;  // LDS OUT buffer per workgroup (entries)
 constexpr uint64_t KEY_MASK = (1ull << KEY_BITS) - 1;
@@ -656,7 +662,7 @@ __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
   __shared__ uint64_t s_q[LQ];  // item ring
   __shared__ uint64_t s_o[LO];  // OUT buffer
   __shared__ uint64_t s_ops[PS_MAX];
-  __shared__ unsigned s_qh, s_qt, s_push, s_on, s_n, s_src, s_ring;
+  __shared__ unsigned s_qh, s_qt, s_push, s_on, s_n, s_src, s_ring, s_ft;
   __shared__ unsigned long long s_f, s_fend, s_g0, s_base;
   __shared__ int s_abort, s_state;
   PartCtl* const ctl = r.ctl;
@@ -670,7 +676,9 @@ __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
     const StepArgs& a = r.steps[t - r.t0];
     FlowSet* const cs = &r.sets[t % 3];
     FlowSet* const ps = &r.sets[(t + 2) % 3];
-    const uint64_t nf = ld_agent(&ps->outc);
+    // |F|: the previous step's OUT count, which counts the appends that overflowed the list too
+    // (PF_OVERFLOW is set then and the host discards the run): never read beyond the list
+    const uint64_t nf = min<uint64_t>(ld_agent(&ps->outc), r.list_cap);
     if (nf == 0 && t > 0) break;  // step t - 1 returned an empty frontier (every workgroup sees it)
     if (lead) {  // the next step's counters (last used by step t - 2, read by step t - 1 at its start)
       FlowSet* const nx = &r.sets[(t + 1) % 3];
@@ -702,18 +710,22 @@ __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
         s_ring = 0;
         if (s_f < s_fend) {
           s_src = 0;
-          s_n = (unsigned)min<uint64_t>(FL, s_fend - s_f);
+          s_ft = flow_ft(s_fend - s_f);
+          s_n = (unsigned)min<uint64_t>(FL / s_ft, s_fend - s_f);
         } else if (s_qt != s_qh) {
           s_src = 1;
-          s_n = min(FL, (int)(s_qt - s_qh));
+          s_ft = flow_ft(s_qt - s_qh);
+          s_n = min(FL / s_ft, s_qt - s_qh);
         } else {
           s_src = 2;
           s_n = 0;
           for (long k = 0;; ++k) {  // idle: claim from Q, or see the step finished
             const unsigned long long h = ld_agent(&cs->head), tl = ld_agent(&cs->tail);
             if (tl > h) {
-              const unsigned m = (unsigned)min<unsigned long long>(FL, tl - h);
+              const unsigned ft = flow_ft(tl - h);
+              const unsigned m = (unsigned)min<unsigned long long>(FL / ft, tl - h);
               if (atomicCAS(&cs->head, h, h + m) == h) {
+                s_ft = ft;
                 s_g0 = h;
                 s_n = m;
                 break;
@@ -741,13 +753,15 @@ __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
       const unsigned long long f0 = s_f, g0 = s_g0;
       uint64_t c = 0;
       bool item = false;
-      if ((unsigned)tid < n) {
+      const unsigned ft = s_ft;
+      const unsigned it = (unsigned)tid / ft, half = (unsigned)tid % ft;  // this thread's item, its part
+      if (it < n) {
         if (src == 0) {  // written in this launch by the previous step: read past the caches
-          c = ld_agent(&F[f0 + tid]), item = true;
+          c = ld_agent(&F[f0 + it]), item = true;
         } else if (src == 1) {
-          c = s_q[(qh0 + tid) & (LQ - 1)], item = true;
-        } else if (g0 + tid < r.qcap) {
-          const uint64_t* q = &r.Q[g0 + tid];
+          c = s_q[(qh0 + it) & (LQ - 1)], item = true;
+        } else if (g0 + it < r.qcap) {
+          const uint64_t* q = &r.Q[g0 + it];
           uint64_t wv = ld_agent(q);
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (long k = 1; (wv & ~KEY_MASK) != tag; ++k) {  // reserved, not yet written
@@ -769,7 +783,7 @@ __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
       // ring slots free for this pass's children (the same value in every thread): children
       // reserve positions in order, so the ones that fit are a prefix of the reservations
       const unsigned qfree = (unsigned)LQ - (qt0 - (src == 1 ? qh0 + n : qh0));
-      listed += item;
+      listed += item && half == 0;
       // OUT configs into the LDS buffer (the global list once it is full)
       auto emit_out = [&](uint64_t k, bool keep) {
         if (!keep) return;
@@ -784,7 +798,7 @@ __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
       };
       // a config holding the returning op (frontier only): its image goes to OUT
       {
-        const bool dret[1] = {item && (c & bitj) != 0};
+        const bool dret[1] = {item && half == 0 && (c & bitj) != 0};
         bool dnew[1] = {false};
         if (__any(dret[0])) insert_batch<1>(r.O, r.tmask, &c, bitj, dret, ep, &ctl->flags, dnew);
         emit_out(c & ~bitj, dnew[0]);
@@ -793,7 +807,8 @@ __global__ void __launch_bounds__(FL) part_flow_kernel(FlowArgs r) {
       const bool expand = item && !(c & bitj);
       const int64_t st = (int64_t)(c >> r.mask_bits);
       unsigned ringc = 0;
-      for (int k0 = 0; k0 < wd; k0 += FB) {
+      for (int b0 = 0; b0 < wd; b0 += (int)ft * FB) {  // (a wave-uniform trip count)
+        const int k0 = b0 + (int)half * FB;
         uint64_t ks[FB];
         bool hs[FB], hj[FB], nw[FB], on[FB];
         bool anyh = false;
