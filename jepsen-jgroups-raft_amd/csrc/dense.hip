@@ -1114,6 +1114,30 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   const bool dbl = (p.pipe & PIPE_DBL) && lb <= DENSE_LMAX - 1;
   uint64_t* const B2 = dbl ? B + (1 << (lb - 3)) : B;
   auto tab = [&](int t) { return (t & 1) ? B2 : B; };
+  // the tile's word list (2^(lb-3) words by popcount layer; a step of H < lb - 3 hi bits uses
+  // each layer's first C(H, q): colex order) in LDS beside the table(s) when it fits, as BLOCK
+  // histories do: a word's index is then an LDS read, not a global load, on every word's chain
+  const uint32_t* words = p.words;
+  const uint32_t* wof = wofs;
+  {
+    const int Hm = lb - 3, ntab = (dbl ? 2 : 1) << Hm;
+    if (Hm >= 1 && ntab + (1 << Hm) / 2 + 16 <= (1 << HSOLO)) {
+      uint32_t* lw = reinterpret_cast<uint32_t*>(B + ntab);
+      uint32_t* lo = lw + (1 << Hm);
+      if (tid <= Hm + 1) {
+        uint32_t o = 0;
+        for (int q = 0; q < tid; ++q) o += binom[Hm * BINOM_N + q];
+        lo[tid] = o;
+      }
+      __syncthreads();
+      for (int q = 0; q <= Hm; ++q) {
+        const uint32_t nq = binom[Hm * BINOM_N + q], og = wofs[q], ol = lo[q];
+        for (uint32_t r = (uint32_t)tid; r < nq; r += 1024u) lw[ol + r] = p.words[og + r];
+      }
+      __syncthreads();
+      words = lw, wof = lo;
+    }
+  }
   unsigned long long* const flags = p.flags + base;
   uint32_t* const anyv = p.team_any + p.team_any_off[team];
   // LC_PIPE bit 8: tagged mirror words (two granules per word, TagTab): readers poll the data,
@@ -1184,7 +1208,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     uint32_t pm_l = 0;  // team bits b: pull from tile rank ^ b at this super-layer
     int xs_l = -1;      // tile holding this step's X (previous step returned a team slot)
     if (seg_l) {
-      nq_l = binom[h1.z * BINOM_N + q_l], o_l = wofs[q_l], mo_l = cum[h1.z * BINOM_N + q_l];
+      nq_l = binom[h1.z * BINOM_N + q_l], o_l = wof[q_l], mo_l = cum[h1.z * BINOM_N + q_l];
       mp_l = cum[h2.y * BINOM_N + min(q_l, h2.y)];
       const int jt = h1.x >= lb ? h1.x - lb : -1;
       const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
@@ -1230,7 +1254,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         const int j = rdl(h1.x, i), jp = rdl(h1.y, i), H = rdl(h1.z, i), xs = rdl(xs_l, i);
         const int t = t_ret_old + i;
         if (r >= nq) continue;
-        const uint32_t w = p.words[o + r];
+        const uint32_t w = words[o + r];
         const uint32_t live_loc = live & lmask, lteam = live >> lb;
         if (w & ~(live_loc >> 3)) continue;
         const bool wide = lteam != 0;
@@ -1299,7 +1323,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
 #pragma unroll
     for (int k = 0; k < TW; ++k) {
       const uint32_t r = (uint32_t)tid + 1024u * k;
-      wn[k] = (i >= 0 && r < rdl(nq_l, i)) ? p.words[rdl(o_l, i) + r] : ~0u;
+      wn[k] = (i >= 0 && r < rdl(nq_l, i)) ? words[rdl(o_l, i) + r] : ~0u;
     }
     while (i >= 0) {
       segm &= segm - 1;
@@ -1308,7 +1332,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
 #pragma unroll
       for (int k = 0; k < TW; ++k) {
         const uint32_t r = (uint32_t)tid + 1024u * k;
-        wn2[k] = (i2 >= 0 && r < rdl(nq_l, i2)) ? p.words[rdl(o_l, i2) + r] : ~0u;
+        wn2[k] = (i2 >= 0 && r < rdl(nq_l, i2)) ? words[rdl(o_l, i2) + r] : ~0u;
       }
       const uint32_t nq = rdl(nq_l, i), mo = rdl(mo_l, i), mp = rdl(mp_l, i), pmask = rdl(pm_l, i);
       const uint32_t o = rdl(o_l, i);
@@ -1339,7 +1363,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
           for (int k = 0; k < TW; ++k) {
             const uint32_t r = r0 + 1024u * k, rn = r + 1024u * TW;
             const uint32_t w = wn[k];
-            wn[k] = rn < nq ? p.words[o + rn] : ~0u;
+            wn[k] = rn < nq ? words[o + rn] : ~0u;
             if (r >= nq || (w & ~live_hi)) continue;
             const uint64_t X = tile_fresh ? 0ull : pipe_x(Bp, w, fresh_hi, jp, keep_lo);
             uint64_t R = pull_hi<4>(Bt, zero, w, j, H, ops, foldm);
@@ -1361,7 +1385,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         for (int k = 0; k < TW; ++k) {
           const uint32_t r = r0 + 1024u * k, rn = r + 1024u * TW;
           wl[k] = wn[k];
-          wn[k] = rn < nq ? p.words[o + rn] : ~0u;
+          wn[k] = rn < nq ? words[o + rn] : ~0u;
           ok[k] = r < nq && !(wl[k] & ~live_hi);
         }
 #pragma unroll
@@ -1434,9 +1458,9 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     if (((uint32_t)rank & ~(live >> lb)) == 0) {
       const uint64_t* xsrc = jl >= lb ? mirror(rank | (1 << (jl - lb)), ns - 1) : nullptr;
       for (int q = 0; q <= H; ++q) {
-        const uint32_t nq = binom[H * BINOM_N + q], o = wofs[q], mo = cum[H * BINOM_N + q];
+        const uint32_t nq = binom[H * BINOM_N + q], o = wof[q], mo = cum[H * BINOM_N + q];
         for (uint32_t r = (uint32_t)tid; r < nq; r += 1024u) {
-          const uint32_t w = p.words[o + r];
+          const uint32_t w = words[o + r];
           if (w & ~live_hi) continue;
           const uint64_t X = !xsrc ? pipe_x(tab(ns - 1), w, 0u, jl, ~0ull)
                              : tagged ? TagTab::ld(xsrc, mo + r, tag_of(ns - 1), p.abort)
