@@ -95,8 +95,8 @@ def check_one(model: str, h, init_value: int = 0, max_configs: int = 0, with_con
 
 def check_many(model: str, h, init_value: int = 0, max_configs: int = 0, n_threads: int = 0):
     L = lib()
-    if n_threads <= 0:
-        n_threads = os.cpu_count() or 1
+    if n_threads <= 0:  # the process's CPU share where the environment states it (16 on a GPU box)
+        n_threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count() or 1
     res = (OracleResult * max(h.n_hist, 1))()
     L.oracle_check_many(MODEL[model], init_value, h.n_hist, _p(h.off), _p(h.index),
                         _p(h.process), _p(h.type), _p(h.f), _p(h.v0), _p(h.v1), _p(h.vflags),
