@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <unordered_map>
 
@@ -35,6 +37,7 @@ struct Op {
   int8_t status;  // -1 pending forever, else completion type
   int8_t f, vflags;
   uint8_t slot;
+  uint8_t inword;  // slot policy: chosen for an in-word slot (0..2)
 };
 
 // per-thread scratch, kept across histories (no allocation per history once warm)
@@ -130,7 +133,7 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
         if (cur >= 0) return void(bad = "process invoked while an op was outstanding");
         cur = (int32_t)ops.size();
         op_of[i - b] = cur;
-        ops.push_back(Op{i, a.v0[i], a.v1[i], -1, a.f[i], a.vflags[i], 0});
+        ops.push_back(Op{i, a.v0[i], a.v1[i], -1, a.f[i], a.vflags[i], 0, 0});
       } else if (t == T_OK || t == T_FAIL || t == T_INFO) {
         if (cur < 0) return void(bad = "completion without an outstanding invocation");
         Op& op = ops[cur];
@@ -197,9 +200,34 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
     }
   }
 
-  // ---- RETURN steps with slot assignment (lowest free slot first), operands computed at each
-  // invocation. Error precedence: a model error anywhere, then > 65535 register values, then
-  // > 63 pending ops.
+  // ---- slot policy. Slot labels are arbitrary (a config's mask is a set), so the search's
+  // answers never depend on them, but the dense tables keep slots 0..2 inside a table word: a
+  // RETURN of one of them lets the next step start one super-layer after it, not two (DESIGN
+  // §3.2). The ops that return soonest go there: the most :ok intervals three "machines" can
+  // hold (greedy by completion, best fit), chosen in one pass over the completions. Assignment
+  // below keeps the widths of lowest-free-first (an unchosen op takes an in-word slot whenever
+  // the lowest free other slot would widen the table). LC_SLOTS=lff: lowest free first only.
+  static const bool slots_lff = [] {
+    const char* e = getenv("LC_SLOTS");
+    return e && strcmp(e, "lff") == 0;
+  }();
+  if (!slots_lff) {
+    int64_t mfree[3] = {-1, -1, -1};
+    for (int64_t i = b; i < e; ++i) {
+      if (a.type[i] != T_OK) continue;
+      const int32_t k = op_of[i - b];
+      if (k < 0) continue;
+      Op& op = ops[k];
+      int best = -1;
+      for (int m = 0; m < 3; ++m)
+        if (mfree[m] < op.inv_pos && (best < 0 || mfree[m] > mfree[best])) best = m;
+      if (best >= 0) op.inword = 1, mfree[best] = i;
+    }
+  }
+
+  // ---- RETURN steps with slot assignment (the policy above, else lowest free slot first),
+  // operands computed at each invocation. Error precedence: a model error anywhere, then
+  // > 65535 register values, then > 63 pending ops.
   o.step_slot.resize(n_ok);
   o.step_ninv.resize(n_ok);
   o.step_cmp_idx.resize(n_ok);
@@ -240,7 +268,12 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
         wide = "more than 63 pending ops";
         continue;
       }
-      const int sl = __builtin_ctzll(~used);
+      int sl = __builtin_ctzll(~used);
+      if (!slots_lff && sl < 3) {
+        const int hi = __builtin_ctzll(~(used | 7ull));  // the lowest free slot >= 3
+        const int npend = __builtin_popcountll(used) + 1;
+        if (!op.inword && hi < std::max(npend, 3)) sl = hi;  // (no wider than lowest-free-first)
+      }
       used |= 1ull << sl;
       op.slot = (uint8_t)sl;
       o.live_max = std::max(o.live_max, 64 - __builtin_clzll(used));
