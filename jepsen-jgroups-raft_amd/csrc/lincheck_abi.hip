@@ -460,8 +460,14 @@ struct lc_plan {
         }
         const int r = team_rot < 0 ? lw - lb : std::min(team_rot, lw - lb);
         if (r <= 0) continue;
+        // with the encoder's slot policy the in-word slots 0..2 hold the soonest-returning ops:
+        // they stay in the word, and slots 3..r+2 (the most used of the rest) become the team bits
+        const int keep = rot_keep_inword ? 3 : 0;
         uint32_t perm[32];
-        for (int k = 0; k < 32; ++k) perm[k] = k < lw ? (uint32_t)(k < r ? lw - r + k : k - r) : (uint32_t)k;
+        for (int k = 0; k < 32; ++k)
+          perm[k] = k >= lw || k < keep ? (uint32_t)k
+                    : k < keep + r    ? (uint32_t)(lw - r + (k - keep))
+                                      : (uint32_t)(k - r);
         uint32_t* w = words.data() + sbeg[h];
         uint32_t* const e = words.data() + wcount[h + 1];
         while (w < e) {
@@ -534,6 +540,8 @@ struct lc_plan {
   uint32_t mirror_seq = 0;  // tagged mirrors: launches since the buffer was last zeroed
   int team_rot = -1;       // LC_TEAM_ROT: tile-team slot rotation (build_dense; -1 auto)
   int rot_min_lb = 16;     // LC_TEAM_ROT_LB: auto rotation from this tile size
+  // rotation keeps slots 0..2 in the word (the encoder's slot policy; LC_SLOTS=lff: rotate them too)
+  bool rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
   // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7); by default 14 for
   // a batch plan (four per CU is the cheaper throughput) and 12 for a chain plan, where a MID
   // team's longer step (w14: 7.7 us against 4.9 as a BLOCK team) becomes a chain of its own
