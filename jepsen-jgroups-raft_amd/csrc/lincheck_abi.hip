@@ -89,6 +89,29 @@ struct DevArray {
   T* as() const { return (T*)p; }
 };
 
+// One launch that zeroes a run's small control buffers (instead of a memset each: every
+// hipMemsetAsync is a fill kernel and a host API call of its own, ~8 per dense run)
+struct ZeroSpans {
+  uint32_t* p[8];
+  uint32_t n[8];  // 4-byte words
+  int k = 0;
+  void add(void* ptr, size_t bytes) {
+    p[k] = (uint32_t*)ptr;
+    n[k] = (uint32_t)((bytes + 3) / 4);
+    ++k;
+  }
+};
+__global__ void __launch_bounds__(256) zero_spans_kernel(ZeroSpans z) {
+  const uint32_t stride = gridDim.x * 256u;
+  for (int s = 0; s < z.k; ++s)
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < z.n[s]; i += stride) z.p[s][i] = 0u;
+}
+hipError_t zero_spans(const ZeroSpans& z, hipStream_t s) {
+  if (z.k == 0) return hipSuccess;
+  hipLaunchKernelGGL(zero_spans_kernel, dim3(32), dim3(256), 0, s, z);
+  return hipGetLastError();
+}
+
 }  // namespace
 }  // namespace lc
 
@@ -133,6 +156,13 @@ struct lc_plan {
   struct StepBytes { double lds, hbm; };
   std::vector<StepBytes> dalg;     // per dense step: algorithmic bytes
   std::vector<int64_t> dalg_off;    // [n_hist + 1] first step of each history in dalg
+  std::vector<StepBytes> dalg_tot;  // [n_hist] every step's (a history that passes runs them all)
+  // team layout last uploaded by run_dense (one launch): unchanged across runs of a plan
+  std::vector<int32_t> up_wgteam, up_base, up_hist, up_anyoff;
+  std::vector<int8_t> up_bits, up_lbits;
+  void* up_ptr = nullptr;
+  unsigned long long* hstage = nullptr;  // pinned: the run's results, copied in one go
+  size_t hstage_bytes = 0;
   int64_t dstream_words = 0;
   int dgrid_b = 0, dgrid_w = 0, dgrid_m = 0;
   int tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX;  // LC_TILE_WGS / LC_DENSE_MAXW (tests)
@@ -180,6 +210,7 @@ struct lc_plan {
     if (stream2) hipStreamDestroy(stream2);
     if (stream3) hipStreamDestroy(stream3);
     if (stream) hipStreamDestroy(stream);
+    if (hstage) hipHostFree(hstage);
   }
 
   void flag_wide() {
@@ -346,6 +377,7 @@ struct lc_plan {
   }
   // bytes of the steps history h ran (all of them, or up to its failing step)
   StepBytes dense_hist_bytes(int h, int fail_t) const {
+    if (fail_t < 0 && h < (int)dalg_tot.size()) return dalg_tot[h];
     StepBytes b{0, 0};
     const int64_t e = fail_t >= 0 ? std::min(dalg_off[h] + fail_t + 1, dalg_off[h + 1]) : dalg_off[h + 1];
     for (int64_t i = dalg_off[h]; i < e; ++i) b.lds += dalg[i].lds, b.hbm += dalg[i].hbm;
@@ -429,6 +461,11 @@ struct lc_plan {
       for (int h = 0; h < n; h += nt) fill(h);
       for (auto& t : th) t.join();
     }
+    dalg_tot.assign(n, StepBytes{0, 0});
+    for (int h = 0; h < n; ++h)
+      for (int64_t i = dalg_off[h]; i < dalg_off[h + 1]; ++i)
+        dalg_tot[h].lds += dalg[i].lds, dalg_tot[h].hbm += dalg[i].hbm;
+    up_ptr = nullptr;  // (a new layout: upload the team tables again)
     for (int h = 0; h < n; ++h) {
       if (!ok[h]) continue;
       const int lw = enc.live_max[h];
@@ -638,9 +675,10 @@ struct lc_plan {
     const int n = enc.n_hist;
     // one stats block per kernel: big, wave, MID
     HIP_TRY(d_stats.ensure(3 * SS_N * 8));
-    HIP_TRY(hipMemsetAsync(d_dqueue.p, 0, 16, stream));
-    HIP_TRY(hipMemsetAsync(d_stats.p, 0, 3 * SS_N * 8, stream));
-    HIP_TRY(hipMemsetAsync(d_dexpl.p, 0, (size_t)std::max(n, 1) * 8, stream));
+    ZeroSpans z0;  // (one launch; the abort word joins it below)
+    z0.add(d_dqueue.p, 16);
+    z0.add(d_stats.p, 3 * SS_N * 8);
+    z0.add(d_dexpl.p, (size_t)std::max(n, 1) * 8);
     DenseParams p{};
     p.sbeg = d_dsbeg.as<int64_t>();
     p.nsteps = d_dnsteps.as<int32_t>();
@@ -744,8 +782,9 @@ struct lc_plan {
       HIP_TRY(d_tbits.ensure(max_teams));
       HIP_TRY(d_tlbits.ensure(max_teams));
       HIP_TRY(d_thist.ensure(max_teams * 4));
-      HIP_TRY(hipMemsetAsync(d_abort.p, 0, 16, stream));
+      z0.add(d_abort.p, 16);
     }
+    HIP_TRY(zero_spans(z0, stream));
     // LC_PIPE bit 6 (default): WAVE histories run on the big kernel's waves after its BLOCK queue
     const bool wave_in_big = (dense_pipe & 64) != 0;
     HIP_TRY(hipEventRecord(ev0, stream));
@@ -799,17 +838,33 @@ struct lc_plan {
         q.queue_w = d_dqueue.as<int32_t>() + 1;
       }
       if (nt) {
-        HIP_TRY(hipMemcpyAsync(d_wgteam.p, l_wgteam[l].data(), twgs * 4, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipMemcpyAsync(d_tbase.p, l_base[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipMemcpyAsync(d_tbits.p, l_bits[l].data(), nt, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipMemcpyAsync(d_tlbits.p, l_lbits[l].data(), nt, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipMemcpyAsync(d_thist.p, l_hist[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipMemsetAsync(d_tflags.p, 0, (size_t)twgs * 8, stream));
-        HIP_TRY(hipMemsetAsync(d_tdone.p, 0, (size_t)twgs * 8, stream));
+        // the team tables: uploaded when the layout (or a buffer) changed, else still in place
+        // from the last run of this plan (one launch)
+        const bool same = launches.size() == 1 && up_ptr == d_wgteam.p && up_wgteam == l_wgteam[l] &&
+                          up_base == l_base[l] && up_bits == l_bits[l] && up_lbits == l_lbits[l] &&
+                          up_hist == l_hist[l] && up_anyoff == l_anyoff[l] && d_tbase.p && d_tanyoff.p;
+        if (!same) {
+          HIP_TRY(hipMemcpyAsync(d_wgteam.p, l_wgteam[l].data(), twgs * 4, hipMemcpyHostToDevice, stream));
+          HIP_TRY(hipMemcpyAsync(d_tbase.p, l_base[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
+          HIP_TRY(hipMemcpyAsync(d_tbits.p, l_bits[l].data(), nt, hipMemcpyHostToDevice, stream));
+          HIP_TRY(hipMemcpyAsync(d_tlbits.p, l_lbits[l].data(), nt, hipMemcpyHostToDevice, stream));
+          HIP_TRY(hipMemcpyAsync(d_thist.p, l_hist[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
+          HIP_TRY(hipMemcpyAsync(d_tanyoff.p, l_anyoff[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
+          if (launches.size() == 1) {
+            up_wgteam = l_wgteam[l], up_base = l_base[l], up_bits = l_bits[l], up_lbits = l_lbits[l];
+            up_hist = l_hist[l], up_anyoff = l_anyoff[l];
+            up_ptr = d_wgteam.p;
+          } else {
+            up_ptr = nullptr;
+          }
+        }
+        ZeroSpans zt;
+        zt.add(d_tflags.p, (size_t)twgs * 8);
+        zt.add(d_tdone.p, (size_t)twgs * 8);
+        zt.add(d_ctl.p, (size_t)nt * dense_ctl_bytes());
+        zt.add(d_tany.p, std::max<size_t>(max_anyw, 1) * 4);
+        HIP_TRY(zero_spans(zt, stream));
         q.done = d_tdone.as<unsigned long long>();
-        HIP_TRY(hipMemsetAsync(d_ctl.p, 0, (size_t)nt * dense_ctl_bytes(), stream));
-        HIP_TRY(hipMemcpyAsync(d_tanyoff.p, l_anyoff[l].data(), nt * 4, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipMemsetAsync(d_tany.p, 0, std::max<size_t>(max_anyw, 1) * 4, stream));
         q.team_any = d_tany.as<uint32_t>();
         q.team_any_off = d_tanyoff.as<int32_t>();
         q.wg_team = d_wgteam.as<int32_t>();
@@ -851,21 +906,32 @@ struct lc_plan {
     float t = 0;
     HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
     *ms += t;
-    if (max_wgs) {
-      int32_t ab = 0;
-      HIP_TRY(hipMemcpy(&ab, d_abort.p, 4, hipMemcpyDeviceToHost));
-      if (ab) {
-        last_error = "dense tile-team watchdog fired (a team workgroup was not resident)";
-        return LC_E_INTERNAL;
-      }
+    // the results (explored, status, fail step, stats, abort word) into one pinned buffer,
+    // copied back-to-back and waited on once
+    const size_t need = (size_t)n * 16 + 3 * SS_N * 8 + 16;
+    if (hstage_bytes < need) {
+      if (hstage) HIP_TRY(hipHostFree(hstage));
+      hstage = nullptr;
+      HIP_TRY(hipHostMalloc(&hstage, need, hipHostMallocDefault));
+      hstage_bytes = need;
     }
-    std::vector<int32_t> st(n), fs(n);
-    std::vector<unsigned long long> ex(n);
-    HIP_TRY(hipMemcpy(st.data(), d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(fs.data(), d_dfail.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(ex.data(), d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost));
-    unsigned long long ss3[3 * SS_N], ss[SS_N];
-    HIP_TRY(hipMemcpy(ss3, d_stats.p, sizeof(ss3), hipMemcpyDeviceToHost));
+    unsigned long long* const ex = hstage;
+    int32_t* const st = reinterpret_cast<int32_t*>(hstage + n);
+    int32_t* const fs = st + n;
+    unsigned long long* const ss3 = reinterpret_cast<unsigned long long*>(fs + n);  // (16 n bytes in)
+    int32_t* const abw = reinterpret_cast<int32_t*>(ss3 + 3 * SS_N);
+    HIP_TRY(hipMemcpyAsync(ex, d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st, d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(fs, d_dfail.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(ss3, d_stats.p, 3 * SS_N * 8, hipMemcpyDeviceToHost, stream));
+    *abw = 0;
+    if (max_wgs) HIP_TRY(hipMemcpyAsync(abw, d_abort.p, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (*abw) {
+      last_error = "dense tile-team watchdog fired (a team workgroup was not resident)";
+      return LC_E_INTERNAL;
+    }
+    unsigned long long ss[SS_N];
     for (int i = 0; i < SS_N; ++i) ss[i] = ss3[i] + ss3[SS_N + i] + ss3[2 * SS_N + i];
     for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
       for (int h : *ids) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
