@@ -532,6 +532,116 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
   }
 }
 
+// ---- REG histories (LC_PIPE bit 10): a WAVE history at most DENSE_REG_LMAX slots wide keeps its
+// whole table in the wave's registers, word w in lane w (2^6 words), and runs history_loop's
+// per-step schedule with lane shuffles for the pulls: no LDS round trip on a word's chain (C1's
+// histories are 5..7 slots wide: ~16 words, a few shuffles per layer).
+constexpr int PIPE_REG = 1024;
+constexpr int REG_LMAX = 9;
+
+// close_in_word with the in-word ops and the returning op's passed by value (no indexed array)
+__device__ __forceinline__ uint64_t close_in_word_r(uint64_t X, uint32_t w, uint32_t live, int j, OpSel o0,
+                                                   OpSel o1, OpSel o2, uint32_t foldm, uint64_t R) {
+  const OpSel lo[3] = {o0, o1, o2};
+  const bool j_lo = j < 3;
+  const uint32_t jh = j_lo ? 0u : 1u << (j - 3);
+  if (w & jh) return R;
+  const uint32_t notj = j_lo ? keep8(j) : 0xffu;
+  const uint64_t notj64 = j_lo ? keep64(j) : ~0ull;
+  R &= notj64;
+  const uint32_t lo_ops = live & 7u & ~(j_lo ? (1u << j) : 0u);
+  const int nlo = __popc(lo_ops);
+  auto lo_step = [&](int k) {
+    if (lo_ops & (1u << k))
+      R |= transfer_lo(lo[k], (foldm >> k) & 1u, X | R, keep8(k) & notj, keep64(k) & notj64, 1 << k);
+  };
+  lo_step(0);
+  lo_step(1);
+  lo_step(2);
+  if (nlo == 3) {
+    lo_step(0);
+    lo_step(1);
+    lo_step(0);
+    lo_step(2);
+  } else if (nlo == 2) {
+    if (lo_ops & 1u) lo_step(0);
+    else lo_step(1);
+  }
+  if (j_lo) {
+    const OpSel oj = j == 0 ? o0 : j == 1 ? o1 : o2;
+    R |= transfer_lo(oj, (foldm >> j) & 1u, X | R, notj, notj64, 1 << j);
+  }
+  return R;
+}
+
+// One REG history h on the calling wave (opt: an LDS op table of the wave, slot k at opt[k]).
+__device__ __forceinline__ void run_regs(const DenseParams& p, int h, OpSel* opt, unsigned long long& st_fout,
+                                         unsigned long long& st_steps) {
+  const int lane = threadIdx.x & 63;
+  const int ns = p.nsteps[h];
+  if (lane < 16) opt[lane] = OpSel{SEL_NONE, SEL_NONE};
+  uint64_t Bw = lane == 0 ? 1ull : 0ull;  // (cas-register) starts at nil, nothing linearized
+  StreamWin sw;
+  int64_t pos = p.sbeg[h];
+  unsigned long long expl = 0;
+  int fail_t = -1;
+  for (int t = 0; t < ns; ++t) {
+    sw.need(p, pos, lane);
+    int ninv;
+    const uint32_t H0 = read_step(sw, pos, lane, true, opt, &ninv);
+    pos += 1 + ninv;
+    const uint32_t live = H0 & DENSE_LIVE_MASK;
+    const int j = (int)((H0 >> DENSE_J_SHIFT) & 31u);
+    const uint32_t foldm = fold_mask(opt);
+    const int L = 32 - __clz((int)live);
+    const int H = L > 3 ? L - 3 : 0;
+    const OpSel o0 = opt[0], o1 = opt[1], o2 = opt[2];
+    OpSel oh[REG_LMAX - 3];
+#pragma unroll
+    for (int b = 0; b < REG_LMAX - 3; ++b) oh[b] = opt[3 + b];
+    const uint32_t w = (uint32_t)lane;
+    const uint32_t jh = j < 3 ? 0u : 1u << (j - 3);
+    const uint32_t pm = (w & jh) ? jh : w;  // bits this word pulls over (only j when it holds j)
+    const bool valid = w < (1u << H) && !(w & ~(live >> 3));
+    const int pc = __popc(w);
+    for (int q = 0; q <= H; ++q) {
+      uint64_t R = 0;
+#pragma unroll
+      for (int b = 0; b < REG_LMAX - 3; ++b) {
+        if (b >= H) break;
+        const uint64_t v = (uint64_t)__shfl_xor((unsigned long long)Bw, 1 << b, 64);
+        if ((pm >> b) & 1u) R |= transfer(oh[b], (foldm >> (b + 3)) & 1u, v);
+      }
+      R = close_in_word_r(Bw, w, live, j, o0, o1, o2, foldm, R);
+      if (valid && pc == q) {
+        expl += (uint32_t)__popcll(R);
+        Bw |= R;
+      }
+    }
+    // return j: B'[m] = B[m | j], B'[m | j] = 0
+    uint64_t nb;
+    if (j >= 3) {
+      const uint64_t v = (uint64_t)__shfl_xor((unsigned long long)Bw, (int)jh, 64);
+      nb = (w & jh) ? 0ull : v;
+    } else {
+      nb = (Bw & ~keep64(j)) >> (1 << j);
+    }
+    Bw = valid ? nb : 0ull;
+    st_fout += (uint32_t)__popcll(Bw);
+    ++st_steps;
+    if (!__any(Bw != 0)) {
+      fail_t = t;
+      break;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
+  if (lane == 0) {
+    p.explored[h] = expl;
+    p.fail_step[h] = fail_t;
+    p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+  }
+}
+
 // ---- pipelined steps (WAVE and BLOCK teams) ---------------------------------------------
 //
 // Consecutive RETURN steps of one history overlap. Step t+1's layer q reads only words of
@@ -646,6 +756,16 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
     const int h = p.order[qi];
     if (p.stamps && tt == 0) p.stamps[4 * h] = __builtin_amdgcn_s_memrealtime();
     const int lmax = p.lmax[h];
+    if constexpr (TEAM == 64) {
+      if ((p.pipe & PIPE_REG) && lmax <= REG_LMAX) {  // the table fits the wave's registers
+        unsigned long long sf = 0, ss = 0;
+        run_regs(p, h, ring[0].ops + OP_PAD, sf, ss);
+        if (tt == 0) st_steps += ss;
+        st_fout += sf;
+        if (p.stamps && tt == 0) p.stamps[4 * h + 1] = __builtin_amdgcn_s_memrealtime();
+        continue;
+      }
+    }
     const int NW = lmax > 3 ? 1 << (lmax - 3) : 1;
     const int ns = p.nsteps[h];
     // double-buffered tables (PIPE_DBL) when two fit the team's LDS: step t on tab(t)

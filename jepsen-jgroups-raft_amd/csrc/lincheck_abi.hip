@@ -175,9 +175,10 @@ struct lc_plan {
   // (no dense_wave_kernel); bit 7 = MID histories (widths 12..mid_maxw) as 4-wave teams inside
   // big workgroups (no dense_mid_kernel); bit 8 = tagged tile-team mirror words (readers poll
   // the data; by default chain plans only); bit 9 = double-buffered tables (a step after an
-  // in-word return starts one super-layer after its predecessor, not two). Default 975 =
-  // 1|2|4|8|64|128|256|512, with the planner.
-  int dense_pipe = 975;
+  // in-word return starts one super-layer after its predecessor, not two); bit 10 = WAVE
+  // histories of at most 9 slots in one wave's registers. Default 1999 =
+  // 1|2|4|8|64|128|256|512|1024, with the planner.
+  int dense_pipe = 1999;
   bool pipe_env = false;  // LC_PIPE given: its bits as they are
   std::vector<int> plan_lb;  // team planner: local slots per tile (0: not a team)
   bool plan_off = false;     // LC_TEAM_PLAN=0: every wide history keeps 17-bit tiles
