@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblincheck.so")
+LIB_PATH = os.environ.get("LC_LIB") or os.path.join(HERE, "liblincheck.so")  # (LC_LIB: an A/B build)
 
 # every symbol include/lincheck.h declares (tests check the exports)
 EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_shard_histories",
