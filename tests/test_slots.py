@@ -1,0 +1,36 @@
+"""The encoder's slot policy (csrc/encode.cpp): the soonest-returning ops take the
+in-word slots 0..2 of the dense tables. Slot labels are arbitrary, so the search's answers never
+depend on them (the GPU tests run every path under the policy); here, on seeded random
+cas-register histories and through the product's encoder itself: the table width of every history
+is the one lowest-free-first gives (the number of ops ever pending at once), and the in-word
+RETURNs never drop below lowest-free-first's in total."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+def test_slot_policy_keeps_widths(tmp_path):
+    exe = tmp_path / "slots"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "sanitize", "slots_main.cpp"),
+                    os.path.join(ROOT, "jepsen-jgroups-raft_amd", "csrc", "encode.cpp"), "-lpthread"], check=True)
+    runs = {}
+    for pol in ("policy", "lff"):
+        env = dict(os.environ)
+        env.pop("LC_SLOTS", None)
+        if pol == "lff":
+            env["LC_SLOTS"] = "lff"
+        out = subprocess.run([str(exe)], capture_output=True, text=True, check=True, env=env, timeout=120).stdout
+        runs[pol] = [tuple(float(x) for x in line.split()) for line in out.splitlines()]
+    a, b = runs["policy"], runs["lff"]
+    assert len(a) == len(b) == 400
+    for ra, rb in zip(a, b):
+        assert ra[0] == rb[0] and ra[3] == rb[3]      # same history, same RETURN steps
+        assert ra[1] == rb[1], (ra, rb)               # same table width
+    assert sum(r[2] for r in a) > sum(r[2] for r in b)  # more in-word RETURNs in total
+    assert sum(r[4] for r in a) <= 1.01 * sum(r[4] for r in b)  # the steps' table work kept
