@@ -568,7 +568,7 @@ def test_gpu_dense_tile_teams_with_step_barriers(monkeypatch):
     p.close()
 
 
-@pytest.mark.parametrize("lbits", ["16", "15", "14"])
+@pytest.mark.parametrize("lbits", ["16", "15", "14", "12"])
 def test_gpu_dense_tile_teams_small_tiles(lbits, monkeypatch):
     """The default (barrier-free) tile-team loop with smaller tiles: up to 2^8 workgroups per
     team, so the "every tile finished step s - 2" check spans several 64-lane chunks."""
