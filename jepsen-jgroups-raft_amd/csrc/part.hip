@@ -501,7 +501,8 @@ __global__ void __launch_bounds__(PL) part_step_kernel(StepArgs a, RunArgs r) {
 // then the new configs its own passes found (an LDS ring: no global claim, no hand-off
 // latency), then, when both are empty, the global overflow queue Q that children go to when a
 // ring is full (tagged words: [epoch | key], polled by the consumer). A pass takes up to FL
-// items (one per thread) and expands them FB candidates at a time: the S probes and, for
+// items with 1, 2 or 3 threads per item (flow_ft: few items at hand, several threads split an
+// item's candidate batches) and expands them FB candidates per thread at a time: the S probes and, for
 // candidates holding the returning op j, the O probes of their images are issued together
 // (every j-holding candidate is in S, new or not, so its image belongs to OUT either way), then
 // the CASes together. New OUT configs collect in an LDS buffer flushed once per step. The step
