@@ -303,6 +303,7 @@ struct lc_plan {
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e), pipe_env = true;
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
     if ((e = getenv("LC_PLAN_K")) && atof(e) > 0) plan_k16 = atof(e);
+    if ((e = getenv("LC_PLAN_X")) && atof(e) > 0) plan_x = atof(e);
     if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
     if ((e = getenv("LC_TEAM_ROT_LB"))) rot_min_lb = atoi(e);
     if ((e = getenv("LC_BATCH_HIST"))) batch_hist = atoi(e);
@@ -592,6 +593,7 @@ struct lc_plan {
   // sweep on C3: 0.4-0.45 -> 11.7 ms, 0.7 -> 13.4-13.6); a plan of a few histories is their
   // chain and keeps a higher factor (C2: 0.7 -> 35.5 ms, 0.4 -> 39.1 ms; rank shares: 1.0, r2cd).
   double plan_k16 = -1;  // < 0: 0.45 for a batch plan, else 1.0 (r2cd)
+  double plan_x = 1.57;  // LC_PLAN_X: the team model's cost per team bit (us per step)
   // A batch plan (LC_BATCH_HIST: more than 600 histories, e.g. C3 on one GPU) fills the chip,
   // so the launch is throughput-bound; fewer histories leave workgroups idle and the launch is
   // its slowest chain (r2rot6-8: C3 1000 keys 11.8 ms batch / 16.2 unrotated; a 250-key share
@@ -603,7 +605,7 @@ struct lc_plan {
     for (uint8_t L : ws) {
       const double k = plan_k16 > 0 ? plan_k16 : batch_plan() ? 0.45 : 1.0;
       t += 1.59 + 0.0043 * k * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
-      if (L > lb) t += 3.87 + 1.57 * (L - lb);
+      if (L > lb) t += 3.87 + plan_x * (L - lb);
     }
     return t;
   }
