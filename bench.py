@@ -323,6 +323,12 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC passes (or absent)")
     args = ap.parse_args()
+    if os.environ.get("LC_MAPS_DUMP"):
+        # diagnosis of exit-time faults: the process's mappings as the interpreter exits (before
+        # the C exit handlers run), so a faulting PC can be mapped to a library and offset
+        import atexit
+        import shutil
+        atexit.register(lambda: shutil.copy("/proc/self/maps", os.environ["LC_MAPS_DUMP"]))
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 1
+#define LC_ABI_VERSION 2  /* 2: lc_failure_configs gained last_op / out_last_op */
 
 enum lc_model { LC_MODEL_CAS_REGISTER = 1, LC_MODEL_COUNTER = 2 };
 enum lc_valid { LC_INVALID = 0, LC_VALID = 1, LC_UNKNOWN = 2 };
@@ -85,6 +85,18 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist,
                  char* err, int32_t err_len);
 
 /*
+ * lc_check keeps one plan per device between calls (device buffers sized to the largest check
+ * so far, streams, occupancy). lc_release frees the cached plan of `device` (< 0: every
+ * device) and its device memory; the next lc_check rebuilds it. A long-lived caller (the JVM)
+ * calls it after a large check; it is never done by a static destructor at process exit.
+ * Not part of the reference interface (Knossos keeps no device state).
+ */
+int32_t lc_release(int32_t device);
+/* Statistics (lc_plan_stats layout, below) of the last lc_check shard run on `device`'s cached
+ * plan; LC_E_ARG when that device has not run one. */
+int32_t lc_check_stats(int32_t device, double* stats, int32_t n);
+
+/*
  * The split lc_check uses for n_gpus > 1 (SURVEY §8(e) axis 1; jepsen.independent's per-key
  * parallelism, register.clj:106): longest-processing-time over n_shards by entry count,
  * out_shard[h] = shard of history h. Host-only (no device needed); deterministic. lc_check
@@ -94,17 +106,24 @@ int32_t lc_shard_histories(int32_t n_hist, const int64_t* hist_off, int32_t n_sh
                            int32_t* out_shard);
 
 /*
- * After lc_check reported history `hist` invalid: up to k configs of the frontier just
- * before the failing :ok (the :configs of a Knossos failure report [ext], compare as a
- * set). Config i: model value state[i] (register: nil when is_nil[i]), and the pending
- * ops it has linearized, as invocation :index values, in linearized[i*64 .. i*64+n_lin[i]).
- * The pending ops themselves (all of them) are written to pending[0..*n_pending).
- * Valid until the next lc_check on this thread. Returns LC_E_CONFIGS when the frontier
- * could not be dumped whole (the verdict stands; only the report is unavailable).
+ * After lc_check reported history `hist` invalid: the frontier just before the failing :ok,
+ * the :configs of a Knossos failure report [ext] (compare as a set; at most k are written, in
+ * a fixed order). Config i: model value state[i] (register: nil when is_nil[i]); the pending
+ * ops it has linearized, as invocation :index values, in linearized[i*64 .. i*64+n_lin[i]) (its
+ * Knossos :pending = the pending ops NOT listed there); last_op[i] = :index of the :ok
+ * completion of the op it linearized last (Knossos's per-config :last-op), -1 for the initial
+ * config. A RETURN's closure stops where the returning op is linearized, so a config it emits
+ * has that op last; a config carried through a RETURN keeps its own; a config reached both
+ * ways takes the most recent. *out_last_op = the most recent last op over the whole frontier
+ * (the report's top-level :last-op). The pending ops themselves (all of them) are written to
+ * pending[0..*n_pending). Valid until the next lc_check on this thread. Returns LC_E_CONFIGS
+ * when the frontier could not be dumped whole (the verdict stands; only the report is
+ * unavailable). Any output pointer may be NULL.
  */
 int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_nil,
-                           int64_t* linearized, int32_t* n_lin, int32_t* n_out,
-                           int64_t* pending, int32_t* n_pending, char* err, int32_t err_len);
+                           int64_t* linearized, int32_t* n_lin, int64_t* last_op, int32_t* n_out,
+                           int64_t* pending, int32_t* n_pending, int64_t* out_last_op, char* err,
+                           int32_t err_len);
 
 /*
  * Counter bounds pre-filter alone: a parallel prefix scan over the

@@ -47,6 +47,16 @@ void set_err(char* err, int32_t len, const char* fmt, ...) {
     }                                                                              \
   } while (0)
 
+// for extern "C" entry points without a plan: message into the caller's err buffer
+#define HIP_CHECK_MSG(expr)                                                        \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      set_err(err, err_len, "%s: %s", #expr, hipGetErrorString(e_));               \
+      return e_ == hipErrorOutOfMemory ? LC_E_MEMORY : LC_E_DEVICE;                \
+    }                                                                              \
+  } while (0)
+
 std::mutex& device_mutex(int dev) {
   static std::mutex mus[64];
   return mus[dev & 63];
@@ -195,6 +205,7 @@ struct lc_plan {
   // uploads, build_dense (reported as stats 20..24)
   double phase_ms[5] = {0};
   int32_t max_t = INT32_MAX;  // failure-frontier dump mode (grid kernel)
+  bool report = false;        // + per-config last-op tags (search.hpp tag_shift; one history)
   int64_t entry_bytes() const { return model == LC_MODEL_CAS_REGISTER ? 8 : 16; }
   int state_bits_of(int h) const {
     return model == LC_MODEL_CAS_REGISTER ? bits_for(enc.n_states[h]) : 0;
@@ -292,6 +303,7 @@ struct lc_plan {
       last_error = "search kernels cannot be resident (occupancy 0)";
       return LC_E_DEVICE;
     }
+    reset_knobs();  // a reused plan (lc_check's per-device cache) must not keep an earlier call's env
     const char* e = getenv("LC_PATH");
     if (e && !strcmp(e, "keys")) path = 1;
     if (e && !strcmp(e, "grid")) path = 2;
@@ -320,6 +332,26 @@ struct lc_plan {
     phase_ms[2] = ms_since(t0);
     return 0;
   }
+
+  // Every env-derived knob back to its default before init_device reads the environment, so a
+  // plan reused across lc_check calls (cached_plan) sees only the current environment. The grid
+  // kernel's capacities keep what earlier runs grew them to (never below the defaults): a
+  // regrow is a whole re-run of the batch.
+  void reset_knobs() {
+    path = 0;
+    tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
+    wide_from = 99, wide_lbits = DENSE_LMAX;
+    dense_pipe = 1999, pipe_env = false, plan_off = false;
+    plan_k16 = -1, plan_x = 1.57, team_rot = -1, rot_min_lb = 16, batch_hist = 600, mid_maxw = 0;
+    rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
+    kfcap = klcap = 1 << 18;
+    cell_cap = 256;
+    ovf_cap = std::max<int64_t>(grown_ovf, 1 << 18);
+    f_cap = std::max(grown_f, 65536);
+    spill_log = std::max(grown_spill, 17);
+  }
+  int64_t grown_ovf = 0;  // capacities run_grid grew (kept across reuses)
+  int grown_f = 0, grown_spill = 0;
 
   int upload_encoded() {
     flag_wide();
@@ -1231,6 +1263,11 @@ struct lc_plan {
     p.mask_bits = bt.mask_bits;
     p.state_shift = bt.mask_bits;
     p.hist_shift = bt.mask_bits + bt.state_bits;
+    p.tag_shift = 0;
+    if (report) {  // one history: the hist field is empty, the 6-bit tag sits above the state
+      p.tag_shift = bt.mask_bits + bt.state_bits;
+      p.hist_shift = p.tag_shift + 6;
+    }
     p.cell_cap = cell_cap;
     p.f_cap = f_cap;
     p.spill_log = spill_log;
@@ -1367,6 +1404,9 @@ struct lc_plan {
         d_ovf.release();
         d_flist.release();
       }
+      grown_ovf = std::max(grown_ovf, ovf_cap);
+      grown_f = std::max(grown_f, f_cap);
+      grown_spill = std::max(grown_spill, spill_log);
       if (rc < 0) return rc;
     }
     return 0;
@@ -1486,12 +1526,17 @@ int plan_build(int device, int model, int64_t init_value, int n_hist, const int6
 }
 
 // lc_check's plan per device, reused from call to call (buffers grow to the largest check);
-// guarded by the device mutex
+// guarded by the device mutex. Never destroyed by a static destructor (at process exit the HIP
+// runtime may be torn down before this library's destructors run): lc_release frees them
+// explicitly, and a process that never calls it leaves them to the OS.
+lc_plan*& cached_slot(int dev) {
+  static lc_plan* plans[64];
+  return plans[dev & 63];
+}
 lc_plan* cached_plan(int dev) {
-  static std::unique_ptr<lc_plan> plans[64];
-  auto& c = plans[dev & 63];
-  if (!c) c.reset(new lc_plan());
-  return c.get();
+  lc_plan*& c = cached_slot(dev);
+  if (!c) c = new lc_plan();
+  return c;
 }
 
 bool valid_args(int model, int n_hist, const int64_t* hist_off, const int32_t* process,
@@ -1765,6 +1810,29 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
   return 0;
 }
 
+int32_t lc_release(int32_t device) {
+  const int ndev = lc_device_count();
+  for (int d = 0; d < std::min(ndev, 64); ++d) {
+    if (device >= 0 && d != device) continue;
+    std::lock_guard<std::mutex> lk(device_mutex(d));
+    lc_plan*& c = cached_slot(d);
+    if (!c) continue;
+    hipSetDevice(d);
+    hipDeviceSynchronize();
+    delete c;
+    c = nullptr;
+  }
+  return 0;
+}
+
+int32_t lc_check_stats(int32_t device, double* stats, int32_t n) {
+  if (device < 0 || device >= 64 || !stats) return LC_E_ARG;
+  std::lock_guard<std::mutex> lk(device_mutex(device));
+  lc_plan* c = cached_slot(device);
+  if (!c) return LC_E_ARG;
+  return lc_plan_stats(c, stats, n);
+}
+
 int32_t lc_shard_histories(int32_t n_hist, const int64_t* hist_off, int32_t n_shards, int32_t* out_shard) {
   if (n_hist < 0 || n_shards < 1 || (n_hist > 0 && (!hist_off || !out_shard))) return LC_E_ARG;
   for (int h = 0; h < n_hist; ++h)
@@ -1774,8 +1842,9 @@ int32_t lc_shard_histories(int32_t n_hist, const int64_t* hist_off, int32_t n_sh
 }
 
 int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_nil,
-                           int64_t* linearized, int32_t* n_lin, int32_t* n_out, int64_t* pending,
-                           int32_t* n_pending, char* err, int32_t err_len) {
+                           int64_t* linearized, int32_t* n_lin, int64_t* last_op, int32_t* n_out,
+                           int64_t* pending, int32_t* n_pending, int64_t* out_last_op, char* err,
+                           int32_t err_len) {
   const LastCheck& L = g_last;
   if (!L.have || hist < 0 || hist + 1 >= (int)L.off.size()) {
     set_err(err, err_len, "no checked history %d on this thread", hist);
@@ -1808,8 +1877,16 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
     return LC_E_ARG;
   }
   const int t_fail = p->fail_step[0];
-  p->max_t = t_fail;  // stop before the failing RETURN: the frontier it saw stays in flist
-  rc = p->run();      // (the grid kernel: the dense tables keep no config lists)
+  if (p->enc.live_max[0] + p->state_bits_of(0) + 6 > 63) {
+    set_err(err, err_len, "failure configs unavailable: %d pending ops leave no room for the last-op tag",
+            p->enc.live_max[0]);
+    return LC_E_CONFIGS;
+  }
+  // stop before the failing RETURN: the frontier it saw stays in flist (the grid kernel: the
+  // dense tables keep no config lists), each config tagged with the step that emitted it
+  p->max_t = t_fail;
+  p->report = true;
+  rc = p->run();
   if (rc) {
     set_err(err, err_len, "%s", p->last_error.c_str());
     return rc;
@@ -1837,43 +1914,67 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
       ++np;
     }
   if (n_pending) *n_pending = np;
-  // read the frontier lists of buffer (t_fail & 1)
+  // read the frontier lists of buffer (t_fail & 1): (config, tag) entries; per config the most
+  // recent tag wins (age = steps since the emitting closure; a carried config is at most
+  // width-many RETURNs old, < 64)
   const lc_plan::Batch& bt = p->batches[0];
   const int par = t_fail & 1;
+  const int tag_shift = bt.mask_bits + bt.state_bits;
   std::vector<uint32_t> fc(2 * p->nwg);
-  hipMemcpy(fc.data(), p->d_fcount.p, fc.size() * 4, hipMemcpyDeviceToHost);
+  HIP_CHECK_MSG(hipMemcpy(fc.data(), p->d_fcount.p, fc.size() * 4, hipMemcpyDeviceToHost));
   const size_t E = (size_t)p->entry_bytes();
   std::vector<uint8_t> buf((size_t)p->f_cap * E);
-  int out = 0;
-  for (int w = 0; w < p->nwg && out < k; ++w) {
+  struct Cfg { uint64_t cfg; int64_t val; int age; };
+  std::vector<Cfg> all;
+  for (int w = 0; w < p->nwg; ++w) {
     const uint32_t n = std::min<uint32_t>(fc[(size_t)par * p->nwg + w], (uint32_t)p->f_cap);
     if (!n) continue;
-    hipMemcpy(buf.data(), (char*)p->d_flist.p + ((size_t)par * p->nwg + w) * p->f_cap * E, n * E,
-              hipMemcpyDeviceToHost);
-    for (uint32_t i = 0; i < n && out < k; ++i) {
+    HIP_CHECK_MSG(hipMemcpy(buf.data(), (char*)p->d_flist.p + ((size_t)par * p->nwg + w) * p->f_cap * E, n * E,
+                            hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i) {
       uint64_t key;
       memcpy(&key, buf.data() + i * E, 8);
       int64_t val = 0;
-      int8_t nil = 0;
-      if (L.model == LC_MODEL_CAS_REGISTER) {
-        const uint64_t sm = (1ull << bt.state_bits) - 1;
-        const int64_t id = (int64_t)((key >> bt.mask_bits) & sm);
-        if (id == 0) nil = 1;
-        else val = en.state_val[en.state_off[0] + id - 1];
-      } else {
-        memcpy(&val, buf.data() + i * E + 8, 8);
-      }
-      int nl = 0;
-      for (int s = 0; s < bt.mask_bits; ++s)
-        if ((key >> s) & 1) {
-          if (linearized) linearized[(size_t)out * 64 + nl] = slot_inv[s];
-          ++nl;
-        }
-      if (state) state[out] = val;
-      if (is_nil) is_nil[out] = nil;
-      if (n_lin) n_lin[out] = nl;
-      ++out;
+      if (L.model == LC_MODEL_COUNTER) memcpy(&val, buf.data() + i * E + 8, 8);
+      const int tag = (int)((key >> tag_shift) & 63);
+      all.push_back({key & ((1ull << tag_shift) - 1), val, (t_fail - 1 - tag) & 63});
     }
+  }
+  // one entry per config (its youngest tag), in config order
+  std::sort(all.begin(), all.end(), [](const Cfg& x, const Cfg& y) {
+    return x.cfg != y.cfg ? x.cfg < y.cfg : x.age < y.age;
+  });
+  all.erase(std::unique(all.begin(), all.end(), [](const Cfg& x, const Cfg& y) { return x.cfg == y.cfg; }),
+            all.end());
+  auto last_index = [&](int age) -> int64_t {  // :ok completion of the emitting step's op
+    const int s = t_fail - 1 - age;
+    return s >= 0 ? en.step_cmp_idx[en.step_off[0] + s] : -1;
+  };
+  int64_t newest = -1;
+  for (const Cfg& c : all) newest = std::max(newest, last_index(c.age));
+  if (out_last_op) *out_last_op = newest;
+  int out = 0;
+  for (const Cfg& c : all) {
+    if (out >= k) break;
+    int64_t val = c.val;
+    int8_t nil = 0;
+    if (L.model == LC_MODEL_CAS_REGISTER) {
+      const uint64_t sm = (1ull << bt.state_bits) - 1;
+      const int64_t id = (int64_t)((c.cfg >> bt.mask_bits) & sm);
+      if (id == 0) nil = 1;
+      else val = en.state_val[en.state_off[0] + id - 1];
+    }
+    int nl = 0;
+    for (int s = 0; s < bt.mask_bits; ++s)
+      if ((c.cfg >> s) & 1) {
+        if (linearized) linearized[(size_t)out * 64 + nl] = slot_inv[s];
+        ++nl;
+      }
+    if (state) state[out] = val;
+    if (is_nil) is_nil[out] = nil;
+    if (n_lin) n_lin[out] = nl;
+    if (last_op) last_op[out] = t_fail == 0 ? -1 : last_index(c.age);
+    ++out;
   }
   if (n_out) *n_out = out;
   return 0;

@@ -129,7 +129,10 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
   const uint32_t nwg = (uint32_t)p.nwg;
   const int nh = p.n_hist;
   const uint64_t mmask = (1ull << p.mask_bits) - 1;
-  const uint64_t smask = (p.hist_shift > p.state_shift) ? ((1ull << (p.hist_shift - p.state_shift)) - 1) : 0;
+  const int state_top = p.tag_shift > 0 ? p.tag_shift : p.hist_shift;  // state bits end here
+  const uint64_t smask = (state_top > p.state_shift) ? ((1ull << (state_top - p.state_shift)) - 1) : 0;
+  const uint64_t tag_clear = p.tag_shift > 0 ? ~(63ull << p.tag_shift) : ~0ull;
+  uint64_t tag_now = 0;  // report mode: this step's tag, already shifted into place
   const size_t fcap = (size_t)p.f_cap;
   const size_t ccap = (size_t)p.cell_cap;
   E* const flist = (E*)p.flist;
@@ -252,7 +255,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
           const int64_t s = (int64_t)((key >> p.state_shift) & smask);
           if (a != -1 && a != s) continue;
           const uint64_t s2 = (uint64_t)(nb >= 0 ? nb : s);
-          ne.key = (key & ~(smask << p.state_shift)) | (s2 << p.state_shift) | (1ull << k);
+          ne.key = (((key & ~(smask << p.state_shift)) | (s2 << p.state_shift) | (1ull << k)) & tag_clear) | tag_now;
         } else {
           // CounterModel.step (counter.clj:102-127): v +/- d, optional pre/post equality
           const uint8_t kind = okd[q];
@@ -266,7 +269,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
           }
           if ((kind & 1) && st != a) continue;
           if ((kind & 2) && r != a) continue;
-          ne.key = key | (1ull << k);
+          ne.key = ((key | (1ull << k)) & tag_clear) | tag_now;
           ne.st = r;
         }
         route(ne, ne.key & ~bj, par);
@@ -351,6 +354,7 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
     int phase = 0;
     for (int t = 0; t < p.max_t; ++t) {
       const int b = t & 1, nb = b ^ 1;
+      if (p.tag_shift > 0) tag_now = (uint64_t)(t & 63) << p.tag_shift;
       // ============================================================ phase X
       uint64_t ts = stamp();
       if (tid == 0) sFcount[nb] = 0;

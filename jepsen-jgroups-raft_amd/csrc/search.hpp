@@ -46,6 +46,11 @@ struct SearchParams {
   int32_t cell_cap, f_cap, spill_log;
   int32_t max_t;  // run steps t < max_t (failure-frontier dumps); INT32_MAX otherwise
   int32_t model;
+  // failure report (one history, lc_failure_configs): > 0 puts a 6-bit tag at this key bit =
+  // the step (mod 64) whose closure emitted the config, kept when a config is carried through a
+  // RETURN; frontier entries then differ by tag too (Knossos's per-config :last-op [ext]).
+  // hist_shift sits above the tag (n_hist == 1). 0: off.
+  int32_t tag_shift;
   // read-only encoded history (see encode.hpp)
   const int32_t* step_beg;   // [n_hist] first global step of each history
   const int32_t* step_end;   // [n_hist] one past its last step

@@ -12,13 +12,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LC_LIB") or os.path.join(HERE, "liblincheck.so")  # (LC_LIB: an A/B build)
 
 # every symbol include/lincheck.h declares (tests check the exports)
-EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_shard_histories",
+EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_release", "lc_check_stats", "lc_shard_histories",
            "lc_failure_configs",
            "lc_counter_bounds", "lc_plan_create", "lc_plan_run", "lc_plan_results",
            "lc_plan_stats", "lc_plan_destroy", "lc_bounds_plan_create", "lc_bounds_plan_sums",
            "lc_bounds_plan_run", "lc_bounds_plan_destroy", "lc_part_create", "lc_part_info",
            "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
            "lc_part_step_end", "lc_part_results", "lc_part_run", "lc_part_destroy")
+ABI_VERSION = 2
 STATS_N = 31
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
@@ -51,9 +52,13 @@ def load():
     L.lc_check.argtypes = [C.c_int32, C.c_int64, C.c_int32] + [P] * 8 + \
         [C.c_int32, C.c_int64, C.c_int32] + [P] * 6 + [C.c_char_p, C.c_int32]
     L.lc_check.restype = C.c_int32
+    L.lc_release.argtypes = [C.c_int32]
+    L.lc_release.restype = C.c_int32
+    L.lc_check_stats.argtypes = [C.c_int32, P, C.c_int32]
+    L.lc_check_stats.restype = C.c_int32
     L.lc_shard_histories.argtypes = [C.c_int32, P, C.c_int32, P]
     L.lc_shard_histories.restype = C.c_int32
-    L.lc_failure_configs.argtypes = [C.c_int32, C.c_int32] + [P] * 7 + [C.c_char_p, C.c_int32]
+    L.lc_failure_configs.argtypes = [C.c_int32, C.c_int32] + [P] * 9 + [C.c_char_p, C.c_int32]
     L.lc_failure_configs.restype = C.c_int32
     L.lc_counter_bounds.argtypes = [C.c_int64, C.c_int32] + [P] * 10 + [C.c_char_p, C.c_int32]
     L.lc_counter_bounds.restype = C.c_int32
@@ -98,7 +103,7 @@ def load():
     L.lc_part_run.restype = C.c_int32
     L.lc_part_destroy.argtypes = [P]
     L.lc_part_destroy.restype = None
-    if L.lc_abi_version() != 1:
+    if L.lc_abi_version() != ABI_VERSION:
         raise LincheckError("ABI version mismatch")
     _lib = L
     return L
@@ -137,6 +142,20 @@ def check(model_kind: int, init_value: int, h, n_gpus: int = 1, max_configs: int
     return out
 
 
+def release(device: int = -1):
+    """lc_release: free lc_check's cached per-device plan(s) and their device memory."""
+    load().lc_release(device)
+
+
+def check_stats(device: int = 0):
+    """lc_check_stats: statistics of the last lc_check run on `device` (Plan.stats() names)."""
+    s = np.zeros(STATS_N, np.float64)
+    rc = load().lc_check_stats(device, _p(s), STATS_N)
+    if rc != 0:
+        raise LincheckError(f"lc_check_stats failed ({rc})")
+    return dict(zip(STATS_NAMES, s.tolist()))
+
+
 def shard_histories(h, n_shards: int) -> np.ndarray:
     """lc_shard_histories: the LPT split lc_check uses over n_shards (host only)."""
     out = np.zeros(max(h.n_hist, 1), np.int32)
@@ -146,25 +165,32 @@ def shard_histories(h, n_shards: int) -> np.ndarray:
     return out[:h.n_hist]
 
 
-def failure_configs(hist: int, k: int = 10):
-    """Pre-failure frontier of history `hist` of the last check() on this thread."""
+def failure_configs(hist: int, k: int = 10, with_last=False):
+    """Pre-failure frontier of history `hist` of the last check() on this thread ->
+    (configs [(value, linearized invocation :index tuple)], pending invocation :index list);
+    with_last: + (per-config :last-op completion :index list, the frontier's newest)."""
     L = load()
     st = np.zeros(k, np.int64)
     nil = np.zeros(k, np.int8)
     lin = np.zeros(k * 64, np.int64)
     nlin = np.zeros(k, np.int32)
+    last = np.zeros(k, np.int64)
     nout = np.zeros(1, np.int32)
     pend = np.zeros(64, np.int64)
     npend = np.zeros(1, np.int32)
+    newest = np.zeros(1, np.int64)
     buf = _errbuf()
-    rc = L.lc_failure_configs(hist, k, _p(st), _p(nil), _p(lin), _p(nlin), _p(nout), _p(pend),
-                              _p(npend), buf, len(buf))
+    rc = L.lc_failure_configs(hist, k, _p(st), _p(nil), _p(lin), _p(nlin), _p(last), _p(nout),
+                              _p(pend), _p(npend), _p(newest), buf, len(buf))
     _raise(rc, buf, "lc_failure_configs")
     cfgs = []
     for i in range(int(nout[0])):
         cfgs.append((None if nil[i] else int(st[i]),
                      tuple(sorted(int(x) for x in lin[i * 64:i * 64 + nlin[i]]))))
-    return cfgs, [int(x) for x in pend[:npend[0]]]
+    pending = [int(x) for x in pend[:npend[0]]]
+    if with_last:
+        return cfgs, pending, [int(x) for x in last[:nout[0]]], int(newest[0])
+    return cfgs, pending
 
 
 def counter_bounds(init_value: int, h):

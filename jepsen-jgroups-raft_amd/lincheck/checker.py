@@ -113,16 +113,20 @@ def _result_map(ops, r, k, model: Model, configs=None) -> Dict[str, Any]:
     if v is False:
         out["op"] = _op_at(ops, int(r["fail_idx"][k]))
         out["previous-ok"] = _op_at(ops, int(r["prev_ok"][k]))
-        # :last-op, the op linearized last before the failure. JIT linearization stops a
-        # RETURN's closure at the returning op, so every config the previous RETURN produced
-        # linearized :previous-ok last (Knossos's README report shows them equal); configs
-        # carried through that RETURN unchanged keep an older last op. Unpinned vs Knossos.
-        out["last-op"] = out["previous-ok"]
         out["invocation"] = _op_at(ops, int(r["fail_inv"][k]))
+        # :last-op: the op linearized last on the way to the pre-failure frontier, from the
+        # search (lc_failure_configs: each config's own, the newest over the frontier here).
+        # Without a report it is :previous-ok's op: a RETURN's closure stops where the
+        # returning op is linearized, so every config the previous RETURN emitted has it last.
+        out["last-op"] = out["previous-ok"]
         if configs is not None:
-            cfgs, pending = configs
-            out["configs"] = [{"model": {"value": s}, "linearized": list(lin),
-                               "pending": pending} for (s, lin) in cfgs]
+            cfgs, pending, lasts, newest = configs
+            out["last-op"] = _op_at(ops, newest)
+            # Knossos :configs [ext]: {:model :last-op :pending}, :pending = the calls this
+            # config has not linearized (invocations, :index order)
+            out["configs"] = [{"model": {"value": s}, "last-op": _op_at(ops, last),
+                               "pending": [_op_at(ops, i) for i in sorted(pending) if i not in lin]}
+                              for (s, lin), last in zip(cfgs, lasts)]
             out["final-paths"] = final_paths(model, cfgs, pending, int(r["fail_inv"][k]), ops)
     return out
 
@@ -155,7 +159,7 @@ class Linearizable(Checker):
             if self.report_configs and r["valid"][k] == 0:
                 # the report is extra: if the frontier dump fails, the verdict still stands
                 try:
-                    cfg = _lib.failure_configs(k, 10)
+                    cfg = _lib.failure_configs(k, 10, with_last=True)
                 except _lib.LincheckError as e:
                     cfg_err = str(e)
             res = _result_map(ops, r, k, self.model, cfg)

@@ -135,12 +135,19 @@ def search(plan, tdist=None, device="cpu", stream=None, max_steps=None, device_l
                     break
                 attempt(plan.absorb, None, n, stream)
                 continue
+            # pack before the count exchange: a rank whose pack overflows then announces zero
+            # counts with its flag, so no peer ever absorbs a stale send buffer
+            n_send = int(counts.sum())
+            send = buf("send", n_send) if n_send else None
+            if n_send:
+                attempt(plan.pack, send, stream)
+            if over:
+                counts, n_send = np.zeros(world, np.int64), 0
             cm, any_over = ex.gather_counts(counts, over)
             if any_over or int(cm.sum()) == 0:
                 break
-            n_send = int(counts.sum())
-            send = buf("send", n_send)
-            attempt(plan.pack, send, stream)
+            if send is None:
+                send = buf("send", 1)
             recv, n_recv = ex.all_to_all(send, n_send, counts.tolist(), cm[:, rank].tolist(),
                                          lambda n: buf("recv", n))
             attempt(plan.absorb, recv, n_recv, stream)

@@ -26,6 +26,7 @@
 
 #include <pthread.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -120,11 +121,13 @@ typedef struct {
   uint64_t mask;
   int64_t value;
   int32_t nil;
+  int32_t last; /* op linearized last on the way here (-1: none); not part of the key */
 } cfg;
 
 typedef struct {
   cfg* keys;
   uint32_t* gen;
+  int64_t* pos; /* optional: per slot, the position of the key in a list (the OUT vector) */
   uint32_t cur;
   int64_t cap, count;
 } cset;
@@ -137,41 +140,52 @@ static uint64_t mix64(uint64_t x) {
 static uint64_t cfg_hash(const cfg* c) {
   return mix64(c->mask * 0x9E3779B97F4A7C15ULL ^ mix64((uint64_t)c->value + (uint64_t)c->nil));
 }
-static int cset_init(cset* s, int64_t cap) {
+static int cset_init2(cset* s, int64_t cap, int with_pos) {
   s->cap = cap; s->count = 0; s->cur = 1;
   s->keys = (cfg*)malloc(sizeof(cfg) * cap);
   s->gen = (uint32_t*)calloc(cap, sizeof(uint32_t));
-  return s->keys && s->gen;
+  s->pos = with_pos ? (int64_t*)malloc(sizeof(int64_t) * cap) : NULL;
+  return s->keys && s->gen && (!with_pos || s->pos);
 }
-static void cset_free(cset* s) { free(s->keys); free(s->gen); }
+static int cset_init(cset* s, int64_t cap) { return cset_init2(s, cap, 0); }
+static void cset_free(cset* s) { free(s->keys); free(s->gen); free(s->pos); }
 static void cset_clear(cset* s) {
   s->count = 0;
   if (++s->cur == 0) { memset(s->gen, 0, sizeof(uint32_t) * s->cap); s->cur = 1; }
 }
-static int cset_insert(cset* s, const cfg* c);
+static int cset_insert_at(cset* s, const cfg* c, int64_t* at);
 static int cset_grow(cset* s) {
   cset n;
-  if (!cset_init(&n, s->cap * 2)) return 0;
+  if (!cset_init2(&n, s->cap * 2, s->pos != NULL)) return 0;
   for (int64_t i = 0; i < s->cap; ++i)
-    if (s->gen[i] == s->cur) cset_insert(&n, &s->keys[i]);
+    if (s->gen[i] == s->cur) {
+      int64_t at;
+      cset_insert_at(&n, &s->keys[i], &at);
+      if (s->pos) n.pos[at] = s->pos[i];
+    }
   cset_free(s);
   *s = n;
   return 1;
 }
-/* returns 1 if inserted (new), 0 if already present, -1 on OOM */
-static int cset_insert(cset* s, const cfg* c) {
+/* returns 1 if inserted (new), 0 if already present, -1 on OOM; *at = the key's slot */
+static int cset_insert_at(cset* s, const cfg* c, int64_t* at) {
   if ((s->count + 1) * 2 > s->cap && !cset_grow(s)) return -1;
   uint64_t m = (uint64_t)s->cap - 1;
   uint64_t h = cfg_hash(c) & m;
   for (;;) {
     if (s->gen[h] != s->cur) {
       s->gen[h] = s->cur; s->keys[h] = *c; s->count++;
+      *at = (int64_t)h;
       return 1;
     }
     const cfg* k = &s->keys[h];
-    if (k->mask == c->mask && k->value == c->value && k->nil == c->nil) return 0;
+    if (k->mask == c->mask && k->value == c->value && k->nil == c->nil) { *at = (int64_t)h; return 0; }
     h = (h + 1) & m;
   }
+}
+static int cset_insert(cset* s, const cfg* c) {
+  int64_t at;
+  return cset_insert_at(s, c, &at);
 }
 
 typedef struct {
@@ -236,7 +250,7 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
                      const int32_t* process, const int8_t* type, const int8_t* f,
                      const int64_t* v0, const int64_t* v1, const int8_t* vflags,
                      int64_t max_configs, oracle_result* out, int64_t cfg_cap,
-                     int64_t* cfg_value, int8_t* cfg_nil, uint64_t* cfg_mask) {
+                     int64_t* cfg_value, int8_t* cfg_nil, uint64_t* cfg_mask, int64_t* cfg_last) {
   memset(out, 0, sizeof(*out));
   out->valid = 1;
   out->fail_idx = out->fail_inv_idx = out->prev_ok_idx = -1;
@@ -308,8 +322,13 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
   int np = 0;
   cvec F = {0}, L = {0}, NL = {0}, OUT = {0};
   cset S, O;
-  if (!cset_init(&S, 1024) || !cset_init(&O, 1024)) { set_err(out, -3, "out of memory"); rc = -3; }
-  cfg c0 = {0, init_value, model_kind == OR_MODEL_CAS_REGISTER ? 1 : 0};
+  /* :last-op per config (only for a failure report, cfg_cap > 0): the op linearized last on the
+   * way to it. A RETURN's closure stops where the returning op is linearized, so every config
+   * it emits has that op last; a config carried through a RETURN (the op was linearized
+   * earlier) keeps its own. Two routes to one config keep the most recent (the closure's). */
+  const int track = cfg_cap > 0;
+  if (!cset_init(&S, 1024) || !cset_init2(&O, 1024, track)) { set_err(out, -3, "out of memory"); rc = -3; }
+  cfg c0 = {0, init_value, model_kind == OR_MODEL_CAS_REGISTER ? 1 : 0, -1};
   if (model_kind == OR_MODEL_CAS_REGISTER) c0.value = 0; /* (cas-register) starts at nil */
   if (!rc) cvec_push(&F, &c0);
   out->max_frontier = 1;
@@ -337,9 +356,13 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
       cfg c = F.v[a];
       if (c.mask >> p & 1) {
         c.mask = squeeze(c.mask, p);
-        int ins = cset_insert(&O, &c);
+        int64_t at;
+        int ins = cset_insert_at(&O, &c, &at);
         if (ins < 0) { rc = -3; break; }
-        if (ins) cvec_push(&OUT, &c);
+        if (ins) {
+          if (track) O.pos[at] = OUT.n;
+          cvec_push(&OUT, &c);
+        }
       } else {
         cvec_push(&L, &c);
       }
@@ -356,7 +379,7 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
                                                          : step_counter(s, &ops[pend_list[k]], &s2, &why);
           if (st == ST_ERROR) { set_err(out, -6, why); rc = -6; break; }
           if (st == ST_INCONSISTENT) continue;
-          cfg c2 = {c->mask | (1ULL << k), s2.value, s2.nil};
+          cfg c2 = {c->mask | (1ULL << k), s2.value, s2.nil, (int32_t)pend_list[k]};
           if (model_kind == OR_MODEL_CAS_REGISTER && s2.nil) c2.value = 0;
           int ins = cset_insert(&S, &c2);
           if (ins < 0) { rc = -3; break; }
@@ -365,9 +388,15 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
           if (k == p) {
             cfg r = c2;
             r.mask = squeeze(r.mask, p);
-            int ins2 = cset_insert(&O, &r);
+            int64_t at;
+            int ins2 = cset_insert_at(&O, &r, &at);
             if (ins2 < 0) { rc = -3; break; }
-            if (ins2) cvec_push(&OUT, &r);
+            if (ins2) {
+              if (track) O.pos[at] = OUT.n;
+              cvec_push(&OUT, &r);
+            } else if (track) {
+              OUT.v[O.pos[at]].last = r.last; /* carried through before: the closure's is newer */
+            }
           } else {
             cvec_push(&NL, &c2);
           }
@@ -395,6 +424,7 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
         if (cfg_value) cfg_value[a] = F.v[a].value;
         if (cfg_nil) cfg_nil[a] = (int8_t)F.v[a].nil;
         if (cfg_mask) cfg_mask[a] = F.v[a].mask;
+        if (cfg_last) cfg_last[a] = F.v[a].last < 0 ? -1 : IDX(ops[F.v[a].last].cmp_pos);
       }
       break;
     }
@@ -431,9 +461,13 @@ static void* many_worker(void* arg) {
     int32_t h = __atomic_fetch_add(&c->next, 1, __ATOMIC_RELAXED);
     if (h >= c->n_hist) break;
     int64_t b = c->hist_off[h], e = c->hist_off[h + 1];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     oracle_check(c->model_kind, c->init_value, e - b, c->index ? c->index + b : NULL,
                  c->process + b, c->type + b, c->f + b, c->v0 + b, c->v1 + b, c->vflags + b,
-                 c->max_configs, &c->out[h], 0, NULL, NULL, NULL);
+                 c->max_configs, &c->out[h], 0, NULL, NULL, NULL, NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    c->out[h].wall_ns = (int64_t)(t1.tv_sec - t0.tv_sec) * 1000000000ll + (t1.tv_nsec - t0.tv_nsec);
   }
   return NULL;
 }

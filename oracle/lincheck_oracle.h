@@ -42,19 +42,21 @@ typedef struct {
   int64_t n_fail_cfgs;    /* |frontier| just before the failing RETURN */
   int32_t n_pending_at_fail;
   int32_t _pad;
+  int64_t wall_ns;        /* oracle_check_many: this history's wall time on its thread */
   int64_t pending_inv_idx[64]; /* invocation :index of each pending op at failure (bit order) */
   char err[128];
 } oracle_result;
 
 /* Check one history. Arrays have n entries; index may be NULL (then position is used).
- * On failure, up to cfg_cap pre-failure configs are written as (value, nil, mask)
- * where mask bit b refers to pending_inv_idx[b]. */
+ * On failure, up to cfg_cap pre-failure configs are written as (value, nil, mask, last)
+ * where mask bit b refers to pending_inv_idx[b] and last is the :index of the :ok completion
+ * of the op the config linearized last (-1: none; Knossos's per-config :last-op [ext]). */
 int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n,
                      const int64_t* index, const int32_t* process, const int8_t* type,
                      const int8_t* f, const int64_t* v0, const int64_t* v1,
                      const int8_t* vflags, int64_t max_configs, oracle_result* out,
                      int64_t cfg_cap, int64_t* cfg_value, int8_t* cfg_nil,
-                     uint64_t* cfg_mask);
+                     uint64_t* cfg_mask, int64_t* cfg_last);
 
 /* Check n_hist concatenated histories (hist_off has n_hist+1 entries) on n_threads
  * POSIX threads (one history per task). */

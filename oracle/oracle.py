@@ -22,7 +22,7 @@ class OracleResult(C.Structure):
                 ("explored", C.c_int64), ("max_frontier", C.c_int64),
                 ("n_returns", C.c_int64), ("final_frontier", C.c_int64),
                 ("n_fail_cfgs", C.c_int64), ("n_pending_at_fail", C.c_int32),
-                ("_pad", C.c_int32), ("pending_inv_idx", C.c_int64 * 64),
+                ("_pad", C.c_int32), ("wall_ns", C.c_int64), ("pending_inv_idx", C.c_int64 * 64),
                 ("err", C.c_char * 128)]
 
     def as_dict(self):
@@ -30,7 +30,8 @@ class OracleResult(C.Structure):
                 "fail_inv_idx": self.fail_inv_idx, "prev_ok_idx": self.prev_ok_idx,
                 "explored": self.explored, "max_frontier": self.max_frontier,
                 "n_returns": self.n_returns, "final_frontier": self.final_frontier,
-                "n_fail_cfgs": self.n_fail_cfgs, "err": self.err.decode()}
+                "n_fail_cfgs": self.n_fail_cfgs, "wall_ns": self.wall_ns,
+                "err": self.err.decode()}
 
 
 _lib = None
@@ -48,7 +49,7 @@ def lib():
         L = C.CDLL(LIB)
         P = C.c_void_p
         L.oracle_check.argtypes = [C.c_int32, C.c_int64, C.c_int64] + [P] * 7 + \
-            [C.c_int64, C.POINTER(OracleResult), C.c_int64, P, P, P]
+            [C.c_int64, C.POINTER(OracleResult), C.c_int64, P, P, P, P]
         L.oracle_check.restype = C.c_int32
         L.oracle_check_many.argtypes = [C.c_int32, C.c_int64, C.c_int32] + [P] * 8 + \
             [C.c_int64, C.c_int32, C.POINTER(OracleResult)]
@@ -77,18 +78,23 @@ def check_one(model: str, h, init_value: int = 0, max_configs: int = 0, with_con
     cv = np.zeros(max(cap, 1), np.int64)
     cn = np.zeros(max(cap, 1), np.int8)
     cm = np.zeros(max(cap, 1), np.uint64)
+    cl = np.zeros(max(cap, 1), np.int64)
     L.oracle_check(MODEL[model], init_value, n, _p(h.index), _p(h.process), _p(h.type),
                    _p(h.f), _p(h.v0), _p(h.v1), _p(h.vflags), max_configs, C.byref(r),
-                   cap, _p(cv), _p(cn), _p(cm))
+                   cap, _p(cv), _p(cn), _p(cm), _p(cl))
     d = r.as_dict()
     if with_configs and r.valid == 0:
         k = min(r.n_fail_cfgs, cap)
         pend = [r.pending_inv_idx[b] for b in range(r.n_pending_at_fail)]
         cfgs = set()
+        last = {}
         for a in range(k):
             lin = tuple(sorted(pend[b] for b in range(len(pend)) if (int(cm[a]) >> b) & 1))
-            cfgs.add((None if cn[a] else int(cv[a]), lin))
+            c = (None if cn[a] else int(cv[a]), lin)
+            cfgs.add(c)
+            last[c] = int(cl[a])
         d["fail_configs"] = cfgs
+        d["fail_last_op"] = last  # config -> :index of its :last-op's :ok completion (-1: none)
         d["pending_inv_idx"] = pend
     return d
 

@@ -170,3 +170,57 @@ def literal_search(model, history, init_value=0):
             last_ok = pos
     return {"valid": True, "fail_pos": -1, "explored": explored, "max_frontier": maxf,
             "prev_ok_pos": -1, "frontier": F}
+
+
+def literal_last_ops(model, history, init_value=0):
+    """Knossos's per-config :last-op [ext], literally: the frontier carries (state, linearized
+    set, last) triples for EVERY route (no dedup on `last`). A RETURN's closure stops where the
+    returning op is linearized, so each config it emits has that op last; a config carried
+    through a RETURN keeps its own. At the first failing :ok -> {(state, frozenset(invocation
+    :index), sorted): set of the :ok completion :index values of every achievable last op (None: the
+    initial config)}; None when the history is valid."""
+    ops = preprocess(history)
+    by_inv = {o["inv"]: k for k, o in enumerate(ops)}
+    by_cmp = {o["cmp"]: k for k, o in enumerate(ops) if o["status"] == "ok"}
+    pending = []
+    F = {(_init(model, init_value), frozenset(), None)}
+
+    def vfor(o):
+        v = o["value"]
+        return tuple(v) if isinstance(v, list) else v
+
+    for pos, o in enumerate(history):
+        if o["type"] == "invoke" and pos in by_inv:
+            pending.append(by_inv[pos])
+        elif o["type"] == "ok":
+            t = by_cmp[pos]
+            out, S, level = set(), set(), []
+            for (s, lin, last) in F:
+                if t in lin:
+                    out.add((s, lin - {t}, last))
+                elif (s, lin) not in S:
+                    level.append((s, lin))
+            while level:
+                nxt = []
+                for (s, lin) in level:
+                    for k in pending:
+                        if k in lin:
+                            continue
+                        s2 = step(model, s, ops[k]["f"], vfor(ops[k]))
+                        if s2 is None or (s2, lin | {k}) in S:
+                            continue
+                        S.add((s2, lin | {k}))
+                        if k == t:
+                            out.add((s2, lin, ops[t]["cmp_index"]))
+                        else:
+                            nxt.append((s2, lin | {k}))
+                level = nxt
+            if not out:
+                res = {}
+                for (s, lin, last) in F:
+                    key = (None if s == NIL else s, tuple(sorted(ops[k]["inv_index"] for k in lin)))
+                    res.setdefault(key, set()).add(last)
+                return res
+            F = out
+            pending.remove(t)
+    return None

@@ -82,9 +82,11 @@ def encode_register(h, hist=0):
 class MockPartPlan:
     H_CAPACITY = -7
 
-    def __init__(self, h, hist=0, rank=0, world=1, set_cap=None):
+    def __init__(self, h, hist=0, rank=0, world=1, set_cap=None, pack_fail_at=None):
         self.rank, self.world = rank, world
         self.set_cap = set_cap  # capacity of this rank's closure set (None: unbounded)
+        self.pack_fail_at = pack_fail_at  # the pack call (0-based) that overflows (None: never)
+        self.packs = self.absorbs = 0
         self.steps, self.mask_bits = encode_register(h, hist)
         self.n_steps = len(self.steps)
         self.err = 0
@@ -126,12 +128,17 @@ class MockPartPlan:
         return np.array([len(s) for s in self.stage], np.int64)
 
     def pack(self, dst, stream=None):
+        self.packs += 1
+        if self.pack_fail_at is not None and self.packs - 1 == self.pack_fail_at:
+            from lincheck._lib import CapacityError
+            raise CapacityError(f"rank {self.rank}: send staging full")
         flat = [x for s in self.stage for x in s]
         # int64 view of the u64 keys (DIRECT is the sign bit)
         dst[:len(flat)] = __import__("torch").tensor(
             np.array(flat, dtype=np.uint64).view(np.int64), dtype=dst.dtype)
 
     def absorb(self, recv, n, stream=None):
+        self.absorbs += 1
         keys = [x for s in self.stage for x in s] if recv is None else \
             [int(x) & M64 for x in recv[:n].tolist()]
         nxt = []

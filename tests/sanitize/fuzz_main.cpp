@@ -82,8 +82,12 @@ int main() {
       errors += enc.err[k] != 0;
       const int64_t b = off[k], n = off[k + 1] - b;
       oracle_result r;
+      // with a failure-report buffer: the per-config :last-op tracking runs under the sanitizers
+      int64_t cv[64], cl[64];
+      int8_t cn[64];
+      uint64_t cm[64];
       oracle_check(model, 0, n, a.index ? a.index + b : nullptr, a.process + b, a.type + b, a.f + b, a.v0 + b,
-                   a.v1 + b, a.vflags + b, 0, &r, 0, nullptr, nullptr, nullptr);
+                   a.v1 + b, a.vflags + b, 0, &r, 64, cv, cn, cm, cl);
       if (r.valid < 0 || r.valid > 2) return 3;
       if ((enc.err[k] != 0) != (r.valid == 2 && r.err_code != 0) && !malformed) return 4;
       invalid += r.valid == 0;

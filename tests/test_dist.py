@@ -172,3 +172,37 @@ def test_partitioned_overflow_on_one_rank_is_collective():
     for r in range(world):
         assert got[r][:2] == [(2, -7), (2, -7)], (r, got[r])
         assert got[r][2] == float(world)
+
+
+def _pack_overflow_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from lincheck import partition
+        from part_mock import MockPartPlan
+        h = _part_histories()[0]
+        # only rank 1 overflows, in its 3rd pack: after it has expanded that level
+        plan = MockPartPlan(h, rank=rank, world=world, pack_fail_at=2 if rank == 1 else None)
+        r = partition.search(plan, tdist, "cpu", None)
+        q.put((rank, (r["valid"], r["err"], plan.absorbs)))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_partitioned_pack_overflow_sends_nothing_stale():
+    """a rank whose pack overflows announces zero counts with its flag in the same
+    count exchange, so no rank runs that level's all-to-all or absorbs a stale send buffer:
+    both ranks stop after the same number of absorbs, with :unknown (LC_H_CAPACITY)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pack_overflow_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][:2] == (2, -7) and got[1][:2] == (2, -7), got
+    assert got[0][2] == got[1][2] > 0, got

@@ -119,6 +119,27 @@ def test_gpu_c4_full_size_grid(monkeypatch):
     assert int(g["explored"][0]) == C4_EXPLORED
 
 
+def test_gpu_lc_check_env_knobs_do_not_stick(monkeypatch):
+    """lc_check reuses one cached plan per device; a knob set for one call
+    (LC_PATH=grid, capacity test hooks) must not carry into the next call without it."""
+    h = synth.gen_register_keys(6, 200, 5, 0.01, config_id=3)
+    monkeypatch.setenv("LC_PATH", "grid")
+    monkeypatch.setenv("LC_CELLCAP", "4")
+    g1 = _lib.check(1, 0, h)
+    assert _lib.check_stats(0)["dense_histories"] == 0
+    monkeypatch.delenv("LC_PATH")
+    monkeypatch.delenv("LC_CELLCAP")
+    g2 = _lib.check(1, 0, h)
+    assert _lib.check_stats(0)["dense_histories"] == h.n_hist
+    for k in g1:
+        assert np.array_equal(g1[k], g2[k]), k
+    _lib.release(0)  # lc_release: the next call rebuilds the cached plan
+    g3 = _lib.check(1, 0, h)
+    assert _lib.check_stats(0)["dense_histories"] == h.n_hist
+    for k in g1:
+        assert np.array_equal(g1[k], g3[k]), k
+
+
 def test_gpu_c4_full_size_dense():
     """C4 on the dense closure tables (the default path since steps carry 24 live slots): a
     pipelined tile team of up to 2^7 workgroups; the same explored count as the grid kernel."""
@@ -195,21 +216,28 @@ def test_gpu_counter_init_value():
         _cmp(g, oracle.check_one("counter", h, init_value=init), 0, f"init={init}")
 
 
-def test_gpu_failure_configs_match_oracle():
-    found = 0
+@pytest.mark.parametrize("m", ["cas-register", "counter"])
+def test_gpu_failure_configs_match_oracle(m):
+    found = carried = 0
+    gen = synth.gen_register if m == "cas-register" else synth.gen_counter
     for t in range(30):
-        h = synth.gen_register(80, 4, 0.1, 9000 + t, invalid=True)
-        g = _lib.check(1, 0, h)
-        e = oracle.check_one("cas-register", h, with_configs=True)
+        h = gen(80, 4, 0.1, 9000 + t, invalid=True)
+        g = _lib.check(KIND[m], 0, h)
+        e = oracle.check_one(m, h, with_configs=True)
         assert int(g["valid"][0]) == e["valid"]
         if e["valid"] != 0:
             continue
-        cfgs, pending = _lib.failure_configs(0, 1 << 12)
+        cfgs, pending, lasts, newest = _lib.failure_configs(0, 1 << 12, with_last=True)
         assert sorted(pending) == sorted(e["pending_inv_idx"])
         assert set(cfgs) == e["fail_configs"]
         assert len(cfgs) == len(e["fail_configs"])
+        # per-config :last-op (Knossos's :configs entries) from the search's tags
+        for c, last in zip(cfgs, lasts):
+            assert last == e["fail_last_op"][c], (t, c, last, e["fail_last_op"][c])
+        assert newest == max(e["fail_last_op"].values())
+        carried += sum(1 for x in lasts if x != e["prev_ok_idx"])
         found += 1
-    assert found > 5
+    assert found > 5 and carried > 0  # some configs were carried through the last RETURN
 
 
 def test_gpu_counter_bounds_vs_oracle():
@@ -357,6 +385,13 @@ def test_checker_api_register_independent():
     lin = r["results"][1]["linear"]
     assert lin["valid?"] is False and lin["op"]["index"] == 7 and lin["previous-ok"]["index"] == 5
     assert lin["configs"] and all(cfg["model"]["value"] == 1 for cfg in lin["configs"])
+    # Knossos-shaped :configs [ext]: {:model :last-op :pending}; the write (index 5) is the only
+    # linearized op, so every config has it last and nothing pending but the failing read
+    for cfg in lin["configs"]:
+        assert set(cfg) == {"model", "last-op", "pending"}
+        assert cfg["last-op"]["index"] == 5 and cfg["last-op"]["type"] == "ok"
+        assert [o["index"] for o in cfg["pending"]] == [6]
+    assert lin["last-op"]["index"] == 5
 
 
 def test_checker_api_counter_kats():

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from brute import brute_first_failure, brute_valid, literal_search
+from brute import brute_first_failure, brute_valid, literal_last_ops, literal_search
 from lincheck import history as H
 from lincheck import synth
 
@@ -116,7 +116,9 @@ def test_check_many_matches_single():
     h = synth.gen_register_keys(16, 100, 5, 0.02, config_id=1)
     many = oracle.check_many("cas-register", h, n_threads=4)
     for k in range(h.n_hist):
-        assert many[k] == oracle.check_one("cas-register", h.sub(k))
+        one = oracle.check_one("cas-register", h.sub(k))
+        assert many[k].pop("wall_ns") > 0 and one.pop("wall_ns") == 0
+        assert many[k] == one
 
 
 def test_counter_bounds_sound():
@@ -133,3 +135,26 @@ def test_counter_bounds_sound():
             rejected += 1
             assert not lin
     assert rejected > 10
+
+
+@pytest.mark.parametrize("model", ["cas-register", "counter"])
+def test_oracle_failure_last_ops_vs_literal(model):
+    """Per-config :last-op of the failure report (Knossos's :configs [ext]): the oracle keeps,
+    per pre-failure config, the most recent op it can have linearized last. Checked against a
+    literal search that carries every route's last op: the oracle's is achievable and is the
+    latest of them. Parity vs Knossos itself is unpinned (no Knossos here)."""
+    n_cfg = n_multi = 0
+    for t in range(200):
+        g = synth.gen_register if model == "cas-register" else synth.gen_counter
+        h = g(30, 4, 0.15, 7000 + t, invalid=True)
+        r = oracle.check_one(model, h, with_configs=True)
+        if r["valid"] != 0:
+            continue
+        lit = literal_last_ops(model, h.to_ops())
+        assert set(lit) == r["fail_configs"]
+        for c, lasts in lit.items():
+            want = max(-1 if x is None else x for x in lasts)
+            assert r["fail_last_op"][c] == want, (t, c, lasts, r["fail_last_op"][c])
+            n_cfg += 1
+            n_multi += len(lasts) > 1
+    assert n_cfg > 50 and n_multi > 0, (n_cfg, n_multi)
