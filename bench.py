@@ -51,25 +51,33 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(h, model: str, budget_s: float, threads: int):
+def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = False):
     """Time the CPU oracle (a C restatement of knossos.linear, test infrastructure) on a
-    bounded sample of the same workload; returns (cpu dict, oracle results, sample keys)."""
+    bounded, FIXED sample of the same workload; returns (cpu dict, oracle results, sample
+    keys, sampled history).
+
+    Many keys: every 20th key (0, 20, ..., 980 for C3: 50 keys, ~20 s of CPU work), checked by
+    `threads` POSIX threads that take keys from a shared counter (dynamic scheduling). The
+    sample does not depend on a timing probe, so two runs check the same keys; the per-key
+    wall times come back from the oracle. `full` checks every key (the whole workload: minutes
+    on C3, whose two heaviest keys take ~2 min each on one core). One history: the longest
+    prefix that fits the budget (the oracle is single-threaded per history, as Knossos is)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (bench cpu_baseline leg only)
     n = h.n_hist
     if n > 1:
-        probe = list(range(min(n, threads)))
-        t0 = time.perf_counter()
-        oracle.check_many(model, h.select(probe), n_threads=threads)
-        dt = max(time.perf_counter() - t0, 1e-3)  # one key per thread ~ per-key latency
-        keys = min(n, max(threads, int(budget_s / dt * threads)))
-        sample = list(range(keys))
+        sample = list(range(n)) if full else list(range(0, n, 20))
         hs = h.select(sample)
         t0 = time.perf_counter()
         res = oracle.check_many(model, hs, n_threads=threads)
         wall = time.perf_counter() - t0
-        desc = f"first {keys} of {n} keys, {threads} threads (one key per thread)"
+        per = np.array([r["wall_ns"] for r in res], np.float64) / 1e9
+        desc = (f"all {n} keys" if full else f"every 20th key ({len(sample)} of {n}: 0, 20, ...)") + \
+            f", {threads} threads taking keys from a shared counter"
         used = threads
+        keys = {"min_s": round(float(per.min()), 4), "median_s": round(float(np.median(per)), 4),
+                "max_s": round(float(per.max()), 3), "sum_s": round(float(per.sum()), 3),
+                "slowest_key": int(sample[int(per.argmax())])}
     else:
         # one history: the oracle is single-threaded like Knossos's per-history search;
         # time the longest prefix that fits the budget, growing from a short one (a wide
@@ -87,10 +95,32 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int):
         sample = [0]
         desc = f"first {hs.n} of {h.n} entries of the single history, 1 thread"
         used = 1
+        keys = None
     ops = hs.n_ops()
-    return ({"value": ops / wall, "unit": "history ops/s", "cores": used, "kind": "port",
-             "sample": desc, "wall_s": round(wall, 3),
-             "configs_per_s": sum(r["explored"] for r in res) / wall}, res, sample, hs)
+    out = {"value": ops / wall, "unit": "history ops/s", "cores": used, "kind": "port",
+           "sample": desc, "wall_s": round(wall, 3),
+           "configs_per_s": sum(r["explored"] for r in res) / wall}
+    if keys is not None:
+        # the sample's wall is max(sum / threads, slowest key): a key's search is one thread
+        keys["ops_per_s_if_perfectly_packed"] = ops / (keys["sum_s"] / threads)
+        out["per_key"] = keys
+    return out, res, sample, hs
+
+
+def whole_workload_cpu(path, workload, threads):
+    """The committed whole-workload CPU run (bench.py --cpu-full on a GPU box, kept under
+    profiles/) for this workload at this thread count, or None."""
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+    except Exception:  # noqa: BLE001
+        return None
+    cb = d.get("cpu_baseline") or {}
+    if not d.get("config", {}).get("workload", "").startswith(workload + ":") or cb.get("cores") != threads:
+        return None
+    return {"value": cb.get("value"), "wall_s": cb.get("wall_s"), "per_key": cb.get("per_key"),
+            "cpu_model": cb.get("cpu_model"), "source": os.path.relpath(path, ROOT)}
 
 
 def bench_c5(args, rank, world, dist, barrier_sync):
@@ -311,6 +341,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=6.0,
                     help="CPU baseline sizing (the 16-key probe underestimates the sample ~2.5x: ~15 s)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="cpu_baseline on every key (the whole workload; minutes on C3)")
+    ap.add_argument("--cpu-whole", default=os.path.join(ROOT, "profiles", "cpu_whole_c3.json"),
+                    help="committed --cpu-full run quoted as cpu_baseline.whole_workload")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="lc_check calls from host arrays timed after the run (0: skip)")
     ap.add_argument("--emulate", default="",
@@ -369,7 +403,7 @@ def main():
     if args.emulate:
         shard_rank, shard_world = (int(x) for x in args.emulate.split("/"))
     if shard_world > 1 and h_all.n_hist > 1:
-        mine = np.flatnonzero(_lib.shard_histories(h_all, shard_world) == shard_rank)
+        mine = np.flatnonzero(_lib.shard_histories_by_cost(kind, 0, h_all, shard_world)[0] == shard_rank)
         h = h_all.select(mine.tolist())
     else:
         h = h_all
@@ -418,10 +452,14 @@ def main():
             ts.append(time.perf_counter() - t0)
         ts.sort()
         med = ts[len(ts) // 2]
-        # (lc_check keeps one plan per device; LC_PHASES=1 prints each call's setup split)
+        # lc_check keeps one plan per device: the last call's setup split (lc_check_stats)
+        cs = _lib.check_stats(local)
         e2e = {"ms_per_check": med * 1e3, "value": h.n_ops() / med, "unit": "history ops/s",
                "reps": args.e2e_reps, "what": "lc_check from host arrays (encode + H2D + search "
                "+ D2H), this rank's histories",
+               "last_call_phases_ms": {k[len("create_"):]: round(cs[k], 3) for k in cs
+                                       if k.startswith("create_")} | {
+                                           "search_kernels": round(cs["kernel_ms"], 3)},
                "first_plan_create_phases_ms": phases}
 
     if dist:
@@ -494,9 +532,26 @@ def main():
     parity = None
     if not args.no_cpu and world == 1 and not args.emulate:
         ci = cpu_info()
-        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, ci["threads"])
+        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, ci["threads"], args.cpu_full)
         cpu.update({k: ci[k] for k in ("cpu_model", "nproc", "affinity")})
         cpu["cores_from"] = ci["share"]
+        if h.n_hist > 1:
+            # the GPU/CPU ratio on the same keys (GPU: the whole workload's check, which
+            # includes these keys; a lower bound on the GPU's speed over the sample)
+            cpu["gpu_over_cpu_same_keys"] = value / cpu["value"]
+            whole = whole_workload_cpu(args.cpu_whole, args.workload, ci["threads"])
+            if whole and whole.get("value"):
+                whole["gpu_over_cpu"] = value / whole["value"]
+                pk = whole.get("per_key") or {}
+                if pk.get("sum_s") and pk.get("max_s"):
+                    # every core this process may use (affinity), from the measured per-key
+                    # times: the wall is at least max(sum / cores, the slowest key) (projection)
+                    whole["projected_all_affinity"] = {
+                        "cores": ci["affinity"],
+                        "value": h.n_ops() / max(pk["sum_s"] / ci["affinity"], pk["max_s"]),
+                        "note": "projection from per-key times, not measured (the box's CPU "
+                                "share is 16 threads)"}
+            cpu["whole_workload"] = whole
         if h.n_hist > 1:
             mism = [k for i, k in enumerate(sample)
                     if int(res["valid"][k]) != ores[i]["valid"] or

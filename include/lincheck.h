@@ -104,6 +104,18 @@ int32_t lc_check_stats(int32_t device, double* stats, int32_t n);
  */
 int32_t lc_shard_histories(int32_t n_hist, const int64_t* hist_off, int32_t n_shards,
                            int32_t* out_shard);
+/*
+ * The split lc_check(n_gpus > 1) uses: longest-processing-time over n_shards by each history's
+ * modeled time (host encode, then the dense kernels' per-step models summed over the history's
+ * RETURN steps: a GPU holding a few hundred keys lasts as long as its slowest chains, and entry
+ * counts say nothing about the frontier width that sets a step's cost). out_cost_us (may be
+ * NULL) receives the model per history. Counter histories balance by entry count. Host only.
+ */
+int32_t lc_shard_histories_by_cost(int32_t model_kind, int64_t init_value, int32_t n_hist,
+                                   const int64_t* hist_off, const int64_t* index, const int32_t* process,
+                                   const int8_t* type, const int8_t* f, const int64_t* v0, const int64_t* v1,
+                                   const int8_t* vflags, int32_t n_shards, int32_t* out_shard,
+                                   double* out_cost_us, char* err, int32_t err_len);
 
 /*
  * After lc_check reported history `hist` invalid: the frontier just before the failing :ok,

@@ -52,21 +52,26 @@
     {:off off :index index :process process :types types :fs fs :v0 v0 :v1 v1 :vflags vflags}))
 
 (defn- failure-configs
-  "lc_failure_configs for history i of the lc_check this thread just made: up to k
-  pre-failure configs as {:model {:value v} :linearized [inv-index ...] :pending [...]},
-  or nil when the frontier could not be dumped (the verdict stands)."
+  "lc_failure_configs (ABI 2) for history i of the lc_check this thread just made: up to k
+  pre-failure configs as {:model {:value v} :linearized [inv-index ...] :last-op ok-index
+  :pending [inv-index ...]} (:pending = every pending op; the config's own are those not in
+  :linearized), plus the frontier's newest last op, or nil when the frontier could not be
+  dumped (the verdict stands)."
   [i k]
   (let [state (long-array k) nils (byte-array k) lin (long-array (* 64 k)) n-lin (int-array k)
-        n-out (int-array 1) pending (long-array 64) n-pending (int-array 1) err (byte-array 512)
+        last-op (long-array k) n-out (int-array 1) pending (long-array 64) n-pending (int-array 1)
+        newest (long-array 1) err (byte-array 512)
         rc (.invokeInt (lib-fn "lc_failure_configs")
-                       (object-array [(int i) (int k) state nils lin n-lin n-out pending n-pending
-                                      err (int 512)]))]
+                       (object-array [(int i) (int k) state nils lin n-lin last-op n-out pending
+                                      n-pending newest err (int 512)]))]
     (when (zero? rc)
       (let [pend (vec (take (aget n-pending 0) pending))]
-        (vec (for [c (range (aget n-out 0))]
-               {:model      {:value (when (zero? (aget nils c)) (aget state c))}
-                :linearized (vec (for [x (range (aget n-lin c))] (aget lin (+ (* 64 c) x))))
-                :pending    pend}))))))
+        {:newest-last-op (aget newest 0)
+         :configs (vec (for [c (range (aget n-out 0))]
+                         {:model      {:value (when (zero? (aget nils c)) (aget state c))}
+                          :linearized (vec (for [x (range (aget n-lin c))] (aget lin (+ (* 64 c) x))))
+                          :last-op    (aget last-op c)
+                          :pending    pend}))}))))
 
 (defn- folded-ops
   "invocation :index -> the op as the model steps it (an :ok completion's :value folded into
@@ -132,15 +137,26 @@
                (= 2 v)    (assoc :error (get err-text (aget errs i) "undecided"))
                (zero? v)  (assoc :op          (at (aget fail i))
                                  :previous-ok (at (aget prev i))
-                                 ;; the op linearized last before the failure: JIT
-                                 ;; linearization returns the previous :ok op last
+                                 ;; without a report: every config the previous RETURN's JIT
+                                 ;; closure emitted has the previous :ok op last
                                  :last-op     (at (aget prev i)))
                (and (zero? v) (:configs opts true))
                ((fn [r]
-                  (let [cfgs (failure-configs i 10)]
-                    (cond-> (assoc r :configs cfgs)
-                      (seq cfgs) (assoc :final-paths
-                                        (final-paths (:model opts) cfgs (aget finv i) ops 10))))))))))))
+                  (if-let [{:keys [configs newest-last-op]} (failure-configs i 10)]
+                    (cond-> (assoc r
+                                   :last-op (at newest-last-op)
+                                   ;; Knossos :configs: {:model :last-op :pending}, :pending =
+                                   ;; the calls this config has not linearized
+                                   :configs (vec (for [c configs
+                                                       :let [lin (set (:linearized c))]]
+                                                   {:model   (:model c)
+                                                    :last-op (at (:last-op c))
+                                                    :pending (vec (for [p (sort (:pending c))
+                                                                        :when (not (lin p))]
+                                                                    (at p)))})))
+                      (seq configs) (assoc :final-paths
+                                           (final-paths (:model opts) configs (aget finv i) ops 10)))
+                    r)))))))))
 
 (defn- model-kind
   "[model_kind init] for the models the GPU implements, else nil (-> Knossos)."

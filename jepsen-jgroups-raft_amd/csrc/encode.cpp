@@ -38,6 +38,8 @@ struct Op {
   int8_t f, vflags;
   uint8_t slot;
   uint8_t inword;  // slot policy: chosen for an in-word slot (0..2)
+  uint8_t kind;    // model operands (computed once, before the assignment pass)
+  int64_t oa, ob;
 };
 
 // per-thread scratch, kept across histories (no allocation per history once warm)
@@ -105,6 +107,9 @@ const char* operands(int model, const Op& op, Find&& find_id, uint8_t& kind, int
   }
 }
 
+// Three passes per history: (1) pairing (knossos.history [ext]) with the slot policy's greedy
+// at each :ok completion, (2) over the ops: the memo (cas-register state ids) and every op's
+// model operands, (3) over the entries: slot assignment and the RETURN steps.
 void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o) {
   thread_local Scratch sc;
   auto IDX = [&](int64_t pos) { return a.index ? a.index[pos] : pos - b; };
@@ -114,10 +119,23 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
     o.msg = m;
     o.n_ops = (int64_t)ops.size();
   };
+  // ---- slot policy. Slot labels are arbitrary (a config's mask is a set), so the search's
+  // answers never depend on them, but the dense tables keep slots 0..2 inside a table word: a
+  // RETURN of one of them lets the next step start one super-layer after it, not two (DESIGN
+  // §3.2). The ops that return soonest go there: the most :ok intervals three "machines" can
+  // hold (greedy by completion, best fit), chosen as the completions arrive in the pairing
+  // pass. Assignment below keeps the widths of lowest-free-first (an unchosen op takes an
+  // in-word slot whenever the lowest free other slot would widen the table). LC_SLOTS=lff:
+  // lowest free first only.
+  static const bool slots_lff = [] {
+    const char* e = getenv("LC_SLOTS");
+    return e && strcmp(e, "lff") == 0;
+  }();
+  int64_t mfree[3] = {-1, -1, -1};
   // ---- pairing (knossos.history [ext])
   ops.clear();
   std::vector<int32_t>& op_of = sc.op_of;
-  op_of.assign(e - b, -1);
+  op_of.resize(e - b);
   // process -> its outstanding op (-1: none): a direct table over [pmin, pmax] when the process
   // ids are dense (Jepsen's are small integers), else open addressing over a power-of-two table
   // (processes are arbitrary int32; a history has at most one per entry)
@@ -133,7 +151,7 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
         if (cur >= 0) return void(bad = "process invoked while an op was outstanding");
         cur = (int32_t)ops.size();
         op_of[i - b] = cur;
-        ops.push_back(Op{i, a.v0[i], a.v1[i], -1, a.f[i], a.vflags[i], 0, 0});
+        ops.push_back(Op{i, a.v0[i], a.v1[i], -1, a.f[i], a.vflags[i], 0, 0, 0, 0, 0});
       } else if (t == T_OK || t == T_FAIL || t == T_INFO) {
         if (cur < 0) return void(bad = "completion without an outstanding invocation");
         Op& op = ops[cur];
@@ -143,6 +161,10 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
           op.v0 = a.v0[i];
           op.v1 = a.v1[i];
           n_ok++;
+          int best = -1;  // slot policy: the machine free latest before this op's invocation
+          for (int m = 0; m < 3; ++m)
+            if (mfree[m] < op.inv_pos && (best < 0 || mfree[m] > mfree[best])) best = m;
+          if (best >= 0) op.inword = 1, mfree[best] = i;
         }
         op_of[i - b] = cur;
         cur = -1;
@@ -170,12 +192,19 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
     });
   }
   if (bad) return fail(LC_H_MALFORMED, bad);
+  if (slots_lff)
+    for (Op& op : ops) op.inword = 0;
   o.n_ops = (int64_t)ops.size();
   // ---- cas-register memo: value -> state id (id 0 = nil), ids in first-appearance order over
-  // the values the register can hold; a linear scan while it has taken few values, then a map
+  // the values the register can hold (ops in invocation order). Values in [0, 64) (Jepsen's
+  // usual domain) through a direct table, others by a linear scan while the register has taken
+  // few values, then a map.
   std::unordered_map<int64_t, int32_t>& sid = sc.sid;
   sid.clear();
+  int32_t small_id[64];
+  std::memset(small_id, 0, sizeof(small_id));
   auto find_id = [&](int64_t v) -> int32_t {  // 0 = not seen
+    if ((uint64_t)v < 64) return small_id[v];
     if (o.state_val.size() <= 32) {
       for (size_t k = 0; k < o.state_val.size(); ++k)
         if (o.state_val[k] == v) return (int32_t)k + 1;
@@ -193,41 +222,28 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
       else continue;
       if (find_id(v)) continue;
       o.state_val.push_back(v);
-      if (o.state_val.size() == 33)  // switch to the map: index every value seen so far
+      const int32_t id = (int32_t)o.state_val.size();
+      if ((uint64_t)v < 64) small_id[v] = id;
+      if (id == 33)  // switch to the map: index every value seen so far
         for (size_t k = 0; k < o.state_val.size(); ++k) sid.emplace(o.state_val[k], (int32_t)k + 1);
-      else if (o.state_val.size() > 33)
-        sid.emplace(v, (int32_t)o.state_val.size());
+      else if (id > 33)
+        sid.emplace(v, id);
     }
   }
-
-  // ---- slot policy. Slot labels are arbitrary (a config's mask is a set), so the search's
-  // answers never depend on them, but the dense tables keep slots 0..2 inside a table word: a
-  // RETURN of one of them lets the next step start one super-layer after it, not two (DESIGN
-  // §3.2). The ops that return soonest go there: the most :ok intervals three "machines" can
-  // hold (greedy by completion, best fit), chosen in one pass over the completions. Assignment
-  // below keeps the widths of lowest-free-first (an unchosen op takes an in-word slot whenever
-  // the lowest free other slot would widen the table). LC_SLOTS=lff: lowest free first only.
-  static const bool slots_lff = [] {
-    const char* e = getenv("LC_SLOTS");
-    return e && strcmp(e, "lff") == 0;
-  }();
-  if (!slots_lff) {
-    int64_t mfree[3] = {-1, -1, -1};
-    for (int64_t i = b; i < e; ++i) {
-      if (a.type[i] != T_OK) continue;
-      const int32_t k = op_of[i - b];
-      if (k < 0) continue;
-      Op& op = ops[k];
-      int best = -1;
-      for (int m = 0; m < 3; ++m)
-        if (mfree[m] < op.inv_pos && (best < 0 || mfree[m] > mfree[best])) best = m;
-      if (best >= 0) op.inword = 1, mfree[best] = i;
+  // every op's operands, in invocation order (the first model error, in that order, wins)
+  for (Op& op : ops) {
+    if (op.status == T_FAIL) continue;  // failed ops never enter the search
+    int64_t oa, ob;
+    if (const char* m = operands(model, op, find_id, op.kind, oa, ob)) {
+      o.live_max = 0;
+      return fail(LC_H_MODEL, m);
     }
+    op.oa = oa, op.ob = ob;
   }
 
-  // ---- RETURN steps with slot assignment (the policy above, else lowest free slot first),
-  // operands computed at each invocation. Error precedence: a model error anywhere, then
-  // > 65535 register values, then > 63 pending ops.
+  // ---- RETURN steps with slot assignment (the policy above, else lowest free slot first).
+  // Error precedence: a model error anywhere (above), then > 65535 register values, then > 63
+  // pending ops.
   o.step_slot.resize(n_ok);
   o.step_ninv.resize(n_ok);
   o.step_cmp_idx.resize(n_ok);
@@ -250,41 +266,34 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
   const char* wide = nullptr;
   uint64_t used = 0;
   int64_t ninv_cur = 0;
-  for (int64_t i = b; i < e; ++i) {
+  int live_max = 0;
+  for (int64_t i = b; i < e && !wide; ++i) {
     const int32_t k = op_of[i - b];
-    if (k < 0) continue;
-    Op& op = ops[k];
+    Op& op = ops[k];  // (every entry belongs to an op once pairing succeeded)
     const int8_t t = a.type[i];
     if (t == T_INVOKE) {
       if (op.status == T_FAIL) continue;  // failed ops never enter the search
-      uint8_t kind;
-      int64_t oa, ob;
-      if (const char* m = operands(model, op, find_id, kind, oa, ob)) {
-        o.live_max = 0;
-        return fail(LC_H_MODEL, m);
-      }
-      if (wide) continue;  // only model errors are still looked for
       if (used == ~0ull >> (64 - MAX_SLOTS)) {
         wide = "more than 63 pending ops";
-        continue;
+        break;
       }
       int sl = __builtin_ctzll(~used);
-      if (!slots_lff && sl < 3) {
+      if (sl < 3 && !op.inword && !slots_lff) {
         const int hi = __builtin_ctzll(~(used | 7ull));  // the lowest free slot >= 3
         const int npend = __builtin_popcountll(used) + 1;
-        if (!op.inword && hi < std::max(npend, 3)) sl = hi;  // (no wider than lowest-free-first)
+        if (hi < std::max(npend, 3)) sl = hi;  // (no wider than lowest-free-first)
       }
       used |= 1ull << sl;
       op.slot = (uint8_t)sl;
-      o.live_max = std::max(o.live_max, 64 - __builtin_clzll(used));
+      live_max = std::max(live_max, 64 - __builtin_clzll(used));
       i_slot[ni] = (uint8_t)sl;
-      i_kind[ni] = kind;
-      i_a[ni] = oa;
-      i_b[ni] = ob;
+      i_kind[ni] = op.kind;
+      i_a[ni] = op.oa;
+      i_b[ni] = op.ob;
       i_index[ni] = IDX(i);  // (the invocation entry itself)
       ++ni;
       ninv_cur++;
-    } else if (t == T_OK && !wide) {
+    } else if (t == T_OK) {
       s_slot[ns] = op.slot;
       s_ninv[ns] = ninv_cur;
       s_cmp[ns] = IDX(i);
@@ -294,6 +303,7 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
       used &= ~(1ull << op.slot);
     }
   }
+  o.live_max = live_max;
   o.step_slot.resize(ns);
   o.step_ninv.resize(ns);
   o.step_cmp_idx.resize(ns);
@@ -320,12 +330,24 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
 
 void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
             const HistArrays& a, Encoded& out) {
-  out = Encoded();
   out.model = model;
   out.n_hist = n_hist;
   out.init_value = init_value;
-  std::vector<OneOut> parts(n_hist);
-  int nt = (int)std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  // per-history parts, kept per calling thread across calls (their buffers keep capacity)
+  thread_local std::vector<OneOut> parts_tl;
+  if ((int)parts_tl.size() < n_hist) parts_tl.resize(n_hist);
+  for (int h = 0; h < n_hist; ++h) {
+    OneOut& o = parts_tl[h];
+    o.err = 0, o.msg.clear(), o.live_max = 0, o.n_states = 1, o.n_ops = 0;
+    o.state_val.clear();
+  }
+  std::vector<OneOut>& parts = parts_tl;
+  static const int nt_max = [] {  // LC_ENC_THREADS: encoder threads (default: the cores, <= 16)
+    const char* e = getenv("LC_ENC_THREADS");
+    const int n = e && atoi(e) > 0 ? atoi(e) : (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(n, 16));
+  }();
+  int nt = nt_max;
   if (hist_off[n_hist] - hist_off[0] < 200000) nt = 1;
   auto run = [&](auto&& fn) {  // fn(h) over every history, nt threads
     std::vector<std::thread> th;

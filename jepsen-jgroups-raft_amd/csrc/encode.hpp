@@ -11,6 +11,7 @@
 // reused after a return; a crashed op keeps its slot forever.
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -33,6 +34,30 @@ struct HistArrays {
   const int8_t* vflags;
 };
 
+// A vector whose resize leaves new elements uninitialised: the encoder writes every element it
+// sizes, and an Encoded reused across calls (lc_check's cached plan) keeps its capacity, so a
+// call neither zero-fills (serially) nor page-faults tens of MB of outputs.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;  // default-initialise: nothing for scalars
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using nvec = std::vector<T, NoInitAlloc<T>>;
+
 struct Encoded {
   int model = 0;
   int n_hist = 0;
@@ -44,24 +69,25 @@ struct Encoded {
   std::vector<int32_t> live_max;   // max concurrently live slots
   std::vector<int32_t> n_states;   // register: distinct states (id 0 = nil)
   std::vector<int64_t> state_off;  // n_hist+1 into state_val (register id -> value, id>=1)
-  std::vector<int64_t> state_val;
+  nvec<int64_t> state_val;
   std::vector<int64_t> n_ops;      // invocations (before :fail removal)
   // per step (all histories concatenated)
-  std::vector<uint8_t> step_slot;     // slot of the returning op
-  std::vector<int64_t> inv_off;       // total_steps+1, into per-invoke arrays
-  std::vector<int64_t> step_cmp_idx;  // :index of the :ok completion
-  std::vector<int64_t> step_inv_idx;  // :index of its invocation
+  nvec<uint8_t> step_slot;     // slot of the returning op
+  nvec<int64_t> inv_off;       // total_steps+1, into per-invoke arrays
+  nvec<int64_t> step_cmp_idx;  // :index of the :ok completion
+  nvec<int64_t> step_inv_idx;  // :index of its invocation
   // per invoke assignment
-  std::vector<uint8_t> inv_slot;
-  std::vector<uint8_t> inv_kind;
-  std::vector<int64_t> inv_a, inv_b;
-  std::vector<int64_t> inv_index;  // :index of the invocation (failure reports)
+  nvec<uint8_t> inv_slot;
+  nvec<uint8_t> inv_kind;
+  nvec<int64_t> inv_a, inv_b;
+  nvec<int64_t> inv_index;  // :index of the invocation (failure reports)
 
   int64_t total_steps() const { return (int64_t)step_slot.size(); }
   int32_t n_steps(int h) const { return step_off[h + 1] - step_off[h]; }
 };
 
 // model: 1 cas-register, 2 counter. Never throws; per-history problems land in err/errmsg.
+// `out` may be reused across calls (its buffers keep their capacity).
 void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
             const HistArrays& a, Encoded& out);
 

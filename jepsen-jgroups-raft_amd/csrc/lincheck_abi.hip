@@ -160,7 +160,16 @@ struct lc_plan {
   DevArray d_kscratch, d_kspill, d_kspillpos, d_kstatus, d_kfail, d_kexplored;
   // dense closure tables (narrow cas-register histories; dense.hpp)
   std::vector<int> dense_b, dense_w, dense_x, dense_m;  // block / wave / wide / mid teams, heaviest first
-  DevArray d_dstream, d_dsbeg, d_dnsteps, d_dlmax, d_dwords, d_dorder, d_dqueue, d_dstatus, d_dfail, d_dexpl;
+  DevArray d_dpack, d_dwords, d_dqueue, d_dstatus, d_dfail, d_dexpl;
+  // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
+  // begin / step count / table width, and the queue order
+  uint32_t* dp_stream = nullptr;
+  int64_t* dp_sbeg = nullptr;
+  int32_t *dp_nst = nullptr, *dp_ord = nullptr;
+  int8_t* dp_lm = nullptr;
+  char* hpack = nullptr;  // pinned staging of d_dpack (kept across calls)
+  size_t hpack_bytes = 0;
+  std::vector<std::vector<uint8_t>> widths;  // per history, per step live width (team planner)
   DevArray d_tany, d_tanyoff, d_tdone;
   DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_tlbits, d_thist;
   struct StepBytes { double lds, hbm; };
@@ -223,6 +232,7 @@ struct lc_plan {
     if (stream3) hipStreamDestroy(stream3);
     if (stream) hipStreamDestroy(stream);
     if (hstage) hipHostFree(hstage);
+    if (hpack) hipHostFree(hpack);
   }
 
   void flag_wide() {
@@ -258,8 +268,9 @@ struct lc_plan {
     }
   }
 
-  template <typename T>
-  int upload(DevArray& d, const std::vector<T>& v) {
+  template <typename V>
+  int upload(DevArray& d, const V& v) {
+    using T = typename V::value_type;
     HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1) * sizeof(T)));
     if (!v.empty()) HIP_TRY(hipMemcpy(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     return 0;
@@ -355,6 +366,19 @@ struct lc_plan {
 
   int upload_encoded() {
     flag_wide();
+    grid_up = false;  // the grid / keys kernels' arrays go up when a run first needs them
+    HIP_TRY(d_queue.ensure(8));
+    auto t0 = std::chrono::steady_clock::now();
+    const int rc = build_dense();
+    phase_ms[4] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+  }
+  bool grid_up = false;
+
+  // the encoded histories as the grid and keys kernels read them (every history; the dense
+  // kernels read only their step streams, so a check the dense tables decide never uploads these)
+  int upload_grid() {
+    if (grid_up) return 0;
     const int n = enc.n_hist;
     std::vector<int64_t> init(n);
     std::vector<int32_t> beg(n), end(n), order(n);
@@ -385,11 +409,8 @@ struct lc_plan {
     if ((rc = upload(d_kshift, ksh))) return rc;
     if ((rc = upload(d_kbits, kbi))) return rc;
     if ((rc = upload(d_order, order))) return rc;
-    HIP_TRY(d_queue.ensure(8));
-    auto t0 = std::chrono::steady_clock::now();
-    rc = build_dense();
-    phase_ms[4] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return rc;
+    grid_up = true;
+    return 0;
   }
 
   // Algorithmic bytes of one dense step with live slots `live` and ninv invocations
@@ -438,12 +459,8 @@ struct lc_plan {
     dense_m.clear();
     if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0 || dgrid_m <= 0) return 0;
     const int n = enc.n_hist;
-    std::vector<uint32_t> words;
-    std::vector<int64_t> sbeg(n, 0);
-    std::vector<int32_t> nst(n, 0);
-    std::vector<int8_t> lm(n, 0);
     std::vector<double> cost(n, 0.0);
-    std::vector<std::vector<uint8_t>> widths(n);  // per step live width (team planner)
+    widths.resize(n);  // per step live width (team planner); inner buffers kept across calls
     plan_lb.assign(n, 0);
     // sizes first (one header per step plus one word per invocation), then every history's
     // stream filled in parallel into its own range
@@ -458,15 +475,35 @@ struct lc_plan {
       dalg_off[h + 1] = dalg_off[h] + (ok[h] ? s1 - s0 : 0);
       wcount[h + 1] = wcount[h] + (ok[h] ? (s1 - s0) + (enc.inv_off[s1] - enc.inv_off[s0]) : 0);
     }
-    words.resize(wcount[n]);
-    dalg.assign(dalg_off[n], StepBytes{0, 0});
+    // everything the dense kernels read goes up in ONE async copy from a pinned staging buffer
+    // (kept across calls: no page faults, DMA at full rate): [words | sbeg | nsteps | order | lmax]
+    const size_t o_sbeg = ((size_t)wcount[n] * 4 + 7) & ~(size_t)7, o_nst = o_sbeg + (size_t)n * 8,
+                 o_ord = o_nst + (size_t)n * 4, o_lm = o_ord + (size_t)n * 4, pack = o_lm + (size_t)n + 8;
+    if (hpack_bytes < pack) {
+      if (hpack) HIP_TRY(hipHostFree(hpack));
+      hpack = nullptr;
+      hpack_bytes = 0;
+      HIP_TRY(hipHostMalloc(&hpack, pack + pack / 4, hipHostMallocDefault));
+      hpack_bytes = pack + pack / 4;
+    }
+    uint32_t* const words = (uint32_t*)hpack;
+    int64_t* const sbeg = (int64_t*)(hpack + o_sbeg);
+    int32_t* const nst = (int32_t*)(hpack + o_nst);
+    int32_t* const ordp = (int32_t*)(hpack + o_ord);
+    int8_t* const lm = (int8_t*)(hpack + o_lm);
+    std::fill(sbeg, sbeg + n, 0);
+    std::fill(nst, nst + n, 0);
+    std::fill(lm, lm + n, 0);
+    dalg.resize(dalg_off[n]);
+    dalg_tot.resize(n);
     auto fill = [&](int h) {
+      dalg_tot[h] = StepBytes{0, 0};
       if (!ok[h]) return;
       sbeg[h] = wcount[h];
       nst[h] = enc.n_steps(h);
       lm[h] = (int8_t)std::max(1, enc.live_max[h]);
       widths[h].resize(nst[h]);
-      uint32_t* out = words.data() + wcount[h];
+      uint32_t* out = words + wcount[h];
       uint32_t live = 0;
       for (int t = 0; t < nst[h]; ++t) {
         const int64_t g = (int64_t)enc.step_off[h] + t;
@@ -484,7 +521,9 @@ struct lc_plan {
         const int L = 32 - __builtin_clz(live);
         cost[h] += (double)(1u << L) * L;
         widths[h][t] = (uint8_t)L;
-        dalg[dalg_off[h] + t] = step_alg_bytes(live, (int)(q1 - q0));
+        const StepBytes sb = step_alg_bytes(live, (int)(q1 - q0));
+        dalg[dalg_off[h] + t] = sb;
+        dalg_tot[h].lds += sb.lds, dalg_tot[h].hbm += sb.hbm;
       }
     };
     {
@@ -495,10 +534,6 @@ struct lc_plan {
       for (int h = 0; h < n; h += nt) fill(h);
       for (auto& t : th) t.join();
     }
-    dalg_tot.assign(n, StepBytes{0, 0});
-    for (int h = 0; h < n; ++h)
-      for (int64_t i = dalg_off[h]; i < dalg_off[h + 1]; ++i)
-        dalg_tot[h].lds += dalg[i].lds, dalg_tot[h].hbm += dalg[i].hbm;
     up_ptr = nullptr;  // (a new layout: upload the team tables again)
     for (int h = 0; h < n; ++h) {
       if (!ok[h]) continue;
@@ -539,8 +574,8 @@ struct lc_plan {
           perm[k] = k >= lw || k < keep ? (uint32_t)k
                     : k < keep + r    ? (uint32_t)(lw - r + (k - keep))
                                       : (uint32_t)(k - r);
-        uint32_t* w = words.data() + sbeg[h];
-        uint32_t* const e = words.data() + wcount[h + 1];
+        uint32_t* w = words + sbeg[h];
+        uint32_t* const e = words + wcount[h + 1];
         while (w < e) {
           const uint32_t x = *w;
           if (x & DENSE_OPW) {
@@ -562,22 +597,26 @@ struct lc_plan {
     std::stable_sort(dense_w.begin(), dense_w.end(), heavy_first);
     std::stable_sort(dense_x.begin(), dense_x.end(), heavy_first);
     std::stable_sort(dense_m.begin(), dense_m.end(), heavy_first);
-    std::vector<int32_t> ord(dense_b.begin(), dense_b.end());
-    ord.insert(ord.end(), dense_w.begin(), dense_w.end());
-    ord.insert(ord.end(), dense_x.begin(), dense_x.end());
-    ord.insert(ord.end(), dense_m.begin(), dense_m.end());
-    dstream_words = (int64_t)words.size();
+    {
+      int32_t* o = ordp;
+      for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
+        o = std::copy(ids->begin(), ids->end(), o);
+    }
+    dstream_words = wcount[n];
+    HIP_TRY(d_dpack.ensure(pack));
+    HIP_TRY(hipMemcpyAsync(d_dpack.p, hpack, pack, hipMemcpyHostToDevice, stream));
+    char* const dp = (char*)d_dpack.p;
+    dp_stream = (uint32_t*)dp;
+    dp_sbeg = (int64_t*)(dp + o_sbeg);
+    dp_nst = (int32_t*)(dp + o_nst);
+    dp_ord = (int32_t*)(dp + o_ord);
+    dp_lm = (int8_t*)(dp + o_lm);
     int rc;
-    if ((rc = upload(d_dstream, words))) return rc;
-    if ((rc = upload(d_dsbeg, sbeg))) return rc;
-    if ((rc = upload(d_dnsteps, nst))) return rc;
-    if ((rc = upload(d_dlmax, lm))) return rc;
     if (!d_dwords.p) {
       std::vector<uint32_t> wl(1u << DENSE_WORD_BITS);
       dense_word_list(DENSE_WORD_BITS, wl.data());
       if ((rc = upload(d_dwords, wl))) return rc;
     }
-    if ((rc = upload(d_dorder, ord))) return rc;
     HIP_TRY(d_dqueue.ensure(16));
     HIP_TRY(d_dstatus.ensure((size_t)std::max(n, 1) * 4));
     HIP_TRY(d_dfail.ensure((size_t)std::max(n, 1) * 4));
@@ -715,11 +754,11 @@ struct lc_plan {
     z0.add(d_stats.p, 3 * SS_N * 8);
     z0.add(d_dexpl.p, (size_t)std::max(n, 1) * 8);
     DenseParams p{};
-    p.sbeg = d_dsbeg.as<int64_t>();
-    p.nsteps = d_dnsteps.as<int32_t>();
-    p.lmax = d_dlmax.as<int8_t>();
+    p.sbeg = dp_sbeg;
+    p.nsteps = dp_nst;
+    p.lmax = dp_lm;
     p.words = d_dwords.as<uint32_t>();
-    p.stream = d_dstream.as<uint32_t>();
+    p.stream = dp_stream;
     p.stream_words = dstream_words;
     p.status = d_dstatus.as<int32_t>();
     p.fail_step = d_dfail.as<int32_t>();
@@ -828,7 +867,7 @@ struct lc_plan {
       HIP_TRY(hipStreamWaitEvent(stream2, ev_fork, 0));
       DenseParams q = p;
       q.n = nw;
-      q.order = d_dorder.as<int32_t>() + nb;
+      q.order = dp_ord + nb;
       q.queue = d_dqueue.as<int32_t>() + 1;
       q.stats = d_stats.as<unsigned long long>() + SS_N;
       HIP_TRY(hipEventRecord(ev_w0, stream2));
@@ -843,7 +882,7 @@ struct lc_plan {
       HIP_TRY(hipStreamWaitEvent(stream3, ev_fork, 0));
       DenseParams q = p;
       q.n = nm;
-      q.order = d_dorder.as<int32_t>() + nb + nw + nx;
+      q.order = dp_ord + nb + nw + nx;
       q.queue = d_dqueue.as<int32_t>() + 2;
       q.stats = d_stats.as<unsigned long long>() + 2 * SS_N;
       HIP_TRY(hipEventRecord(ev_m0, stream3));
@@ -860,16 +899,16 @@ struct lc_plan {
       const int nt = (int)l_base[l].size(), twgs = (int)l_wgteam[l].size();
       DenseParams q = p;
       q.n = l == 0 ? nb : 0;
-      q.order = d_dorder.as<int32_t>();
+      q.order = dp_ord;
       q.queue = d_dqueue.as<int32_t>();
       q.n2 = l == 0 ? nm : 0;
-      q.order2 = d_dorder.as<int32_t>() + nb + nw + nx;
+      q.order2 = dp_ord + nb + nw + nx;
       q.queue2 = d_dqueue.as<int32_t>() + 2;
       q.n_team_wgs = twgs;
       q.n_w = 0;
       if (l == 0 && wave_in_big) {
         q.n_w = nw;
-        q.order_w = d_dorder.as<int32_t>() + nb;
+        q.order_w = dp_ord + nb;
         q.queue_w = d_dqueue.as<int32_t>() + 1;
       }
       if (nt) {
@@ -1435,6 +1474,7 @@ struct lc_plan {
       for (int h : dense_m) done[h] = 1;
     }
     if (keys) {
+      if ((rc = upload_grid())) return rc;
       rc = run_keys(&ms);
       if (rc) return rc;
       for (int h = 0; h < enc.n_hist; ++h)
@@ -1444,6 +1484,7 @@ struct lc_plan {
         if (!enc.err[h] && !done[h]) grid_ids.push_back(h);
     }
     if (!grid_ids.empty()) {
+      if ((rc = upload_grid())) return rc;
       rc = run_grid(grid_ids, &ms);
       if (rc) return rc;
     }
@@ -1577,6 +1618,58 @@ void lpt_shards(int n_hist, const int64_t* off, int G, int32_t* out_shard) {
   }
 }
 
+// Modeled time (us) of each history's dependent chain of RETURN steps on the dense kernels,
+// with the team planner's step models (lc_plan::est_*; MI355X LC_DEBUG fits) as the history
+// would run in a shard of a few hundred keys (a chain plan): WAVE (width <= 11) 7.9 us per
+// step, MID (12..14) 4.9 + 0.0016 * 2^(L-3), BLOCK (15..17) 4.67 + 0.00266 * 2^(L-3), wider a
+// tile team of 16-slot tiles, 1.59 + 0.0043 * 2^(min(L,16)-3) + [L > 16] (3.87 + 1.57 (L-16)).
+// Counter histories and histories the dense tables do not take (the grid kernel) cost their
+// entry count (one unit per entry). Host only.
+void history_costs(int model, int64_t init_value, int n_hist, const int64_t* off, const HistArrays& a,
+                   std::vector<double>& cost) {
+  cost.assign(n_hist, 0.0);
+  if (model != LC_MODEL_CAS_REGISTER) {
+    for (int h = 0; h < n_hist; ++h) cost[h] = (double)(off[h + 1] - off[h]);
+    return;
+  }
+  Encoded enc;
+  encode(model, init_value, n_hist, off, a, enc);
+  for (int h = 0; h < n_hist; ++h) {
+    const int lw = enc.live_max[h];
+    if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || lw > DENSE_WIDE_LMAX) {
+      cost[h] = (double)(off[h + 1] - off[h]);
+      continue;
+    }
+    uint64_t live = 0;
+    double t = 0;
+    for (int64_t g = enc.step_off[h]; g < enc.step_off[h + 1]; ++g) {
+      if (g > enc.step_off[h]) live &= ~(1ull << enc.step_slot[g - 1]);
+      for (int64_t q = enc.inv_off[g]; q < enc.inv_off[g + 1]; ++q) live |= 1ull << enc.inv_slot[q];
+      const int L = live ? 64 - __builtin_clzll(live) : 0;
+      const double w = std::ldexp(1.0, std::max(0, std::min(L, 16) - 3));
+      t += lw <= DENSE_WAVE_LMAX ? 7.9
+           : lw <= 14            ? 4.9 + 0.0016 * w
+           : lw <= DENSE_LMAX    ? 4.67 + 0.00266 * std::ldexp(1.0, std::max(0, L - 3))
+                                 : 1.59 + 0.0043 * w + (L > 16 ? 3.87 + 1.57 * (L - 16) : 0.0);
+    }
+    cost[h] = t;
+  }
+}
+
+// LPT over G shards by cost: heaviest first, each to the least-loaded shard (lowest index on
+// ties); deterministic. Host only.
+void lpt_by_cost(int n_hist, const std::vector<double>& cost, int G, int32_t* out_shard) {
+  std::vector<int> order(n_hist);
+  for (int h = 0; h < n_hist; ++h) order[h] = h;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+  std::vector<double> load(G, 0.0);
+  for (int h : order) {
+    const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    out_shard[h] = g;
+    load[g] += cost[h];
+  }
+}
+
 // state of the most recent lc_check on this thread (for lc_failure_configs)
 struct LastCheck {
   int model = 0, device = 0;
@@ -1703,12 +1796,18 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
     return 0;
   }
 
-  // shard histories over devices: longest-processing-time on entry counts
+  // shard histories over devices: longest-processing-time on each history's modeled chain time
+  // (lc_shard_histories_by_cost; a shard lasts as long as its slowest chains)
   std::vector<std::vector<int>> shard(G);
-  {
+  if (G > 1) {
     std::vector<int32_t> of(n_hist);
-    lpt_shards(n_hist, off0.data(), G, of.data());
+    std::vector<double> cost;
+    history_costs(model_kind, init_value, n_hist, off0.data(),
+                  HistArrays{off0[n_hist], cidx, cpr, cty, cf, cv0, cv1, cvf}, cost);
+    lpt_by_cost(n_hist, cost, G, of.data());
     for (int h = 0; h < n_hist; ++h) shard[of[h]].push_back(h);
+  } else {
+    for (int h = 0; h < n_hist; ++h) shard[0].push_back(h);
   }
   std::vector<int> rcs(G, 0);
   std::vector<std::string> msgs(G);
@@ -1831,6 +1930,29 @@ int32_t lc_check_stats(int32_t device, double* stats, int32_t n) {
   lc_plan* c = cached_slot(device);
   if (!c) return LC_E_ARG;
   return lc_plan_stats(c, stats, n);
+}
+
+int32_t lc_shard_histories_by_cost(int32_t model_kind, int64_t init_value, int32_t n_hist,
+                                   const int64_t* hist_off, const int64_t* index, const int32_t* process,
+                                   const int8_t* type, const int8_t* f, const int64_t* v0, const int64_t* v1,
+                                   const int8_t* vflags, int32_t n_shards, int32_t* out_shard,
+                                   double* out_cost_us, char* err, int32_t err_len) {
+  if (n_shards < 1 || (n_hist > 0 && !out_shard)) {
+    set_err(err, err_len, "n_shards < 1 or out_shard NULL");
+    return LC_E_ARG;
+  }
+  if (!valid_args(model_kind, n_hist, hist_off, process, type, f, v0, v1, vflags, err, err_len))
+    return LC_E_ARG;
+  const int64_t b0 = hist_off[0];
+  std::vector<int64_t> off0(hist_off, hist_off + n_hist + 1);
+  for (auto& x : off0) x -= b0;
+  auto at = [&](auto* ptr) { return ptr ? ptr + b0 : ptr; };
+  HistArrays a{off0[n_hist], at(index), at(process), at(type), at(f), at(v0), at(v1), at(vflags)};
+  std::vector<double> cost;
+  history_costs(model_kind, init_value, n_hist, off0.data(), a, cost);
+  lpt_by_cost(n_hist, cost, n_shards, out_shard);
+  if (out_cost_us) std::copy(cost.begin(), cost.end(), out_cost_us);
+  return 0;
 }
 
 int32_t lc_shard_histories(int32_t n_hist, const int64_t* hist_off, int32_t n_shards, int32_t* out_shard) {

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("LC_LIB") or os.path.join(HERE, "liblincheck.so")  # (
 
 # every symbol include/lincheck.h declares (tests check the exports)
 EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_release", "lc_check_stats", "lc_shard_histories",
+           "lc_shard_histories_by_cost",
            "lc_failure_configs",
            "lc_counter_bounds", "lc_plan_create", "lc_plan_run", "lc_plan_results",
            "lc_plan_stats", "lc_plan_destroy", "lc_bounds_plan_create", "lc_bounds_plan_sums",
@@ -57,6 +58,9 @@ def load():
     L.lc_check_stats.argtypes = [C.c_int32, P, C.c_int32]
     L.lc_check_stats.restype = C.c_int32
     L.lc_shard_histories.argtypes = [C.c_int32, P, C.c_int32, P]
+    L.lc_shard_histories_by_cost.argtypes = [C.c_int32, C.c_int64, C.c_int32] + [P] * 8 + \
+        [C.c_int32, P, P, C.c_char_p, C.c_int32]
+    L.lc_shard_histories_by_cost.restype = C.c_int32
     L.lc_shard_histories.restype = C.c_int32
     L.lc_failure_configs.argtypes = [C.c_int32, C.c_int32] + [P] * 9 + [C.c_char_p, C.c_int32]
     L.lc_failure_configs.restype = C.c_int32
@@ -163,6 +167,19 @@ def shard_histories(h, n_shards: int) -> np.ndarray:
     if rc != 0:
         raise LincheckError(f"lc_shard_histories failed ({rc})")
     return out[:h.n_hist]
+
+
+def shard_histories_by_cost(model_kind: int, init_value: int, h, n_shards: int):
+    """lc_shard_histories_by_cost: the split lc_check(n_gpus) uses -> (shard per history,
+    modeled chain time per history in us). Host only."""
+    out = np.zeros(max(h.n_hist, 1), np.int32)
+    cost = np.zeros(max(h.n_hist, 1), np.float64)
+    buf = _errbuf()
+    rc = load().lc_shard_histories_by_cost(model_kind, init_value, h.n_hist, _p(h.off), _p(h.index),
+                                           _p(h.process), _p(h.type), _p(h.f), _p(h.v0), _p(h.v1),
+                                           _p(h.vflags), n_shards, _p(out), _p(cost), buf, len(buf))
+    _raise(rc, buf, "lc_shard_histories_by_cost")
+    return out[:h.n_hist], cost[:h.n_hist]
 
 
 def failure_configs(hist: int, k: int = 10, with_last=False):

@@ -35,8 +35,8 @@ int main(int argc, char** argv) {
   auto vflags = load<int8_t>(dir, "vflags");
   lc::HistArrays a{(int64_t)type.size(), index.data(), process.data(), type.data(), f.data(),
                    v0.data(), v1.data(), vflags.data()};
+  lc::Encoded e;  // reused across reps, as lc_check's cached plan reuses its own
   for (int r = 0; r < reps; ++r) {
-    lc::Encoded e;
     auto t0 = std::chrono::steady_clock::now();
     lc::encode(1, 0, (int)off.size() - 1, off.data(), a, e);
     auto t1 = std::chrono::steady_clock::now();
