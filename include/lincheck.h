@@ -256,6 +256,18 @@ int32_t lc_part_run(lc_part* p, void* stream, int64_t max_steps, int64_t* out4, 
                     int32_t err_len);
 void lc_part_destroy(lc_part* p);
 
+/* The same search in ONE call for a caller without a collective library (a JVM through JNA):
+ * the n_ranks ranks are threads of this process, rank r on device r % (visible devices); per
+ * BFS level the counts are exchanged in host memory and each receiver pulls its candidates from
+ * every sender's staging segment with peer copies (hipMemcpyPeerAsync over xGMI). Outputs as
+ * lc_check's for one history (n_ranks <= 0: one rank per visible device; 1: lc_part_run).
+ * Frontier capacity grows with the ranks (capacity_log2 per rank, 0 = 22). */
+int32_t lc_part_check(int32_t model_kind, int64_t init_value, int64_t n, const int64_t* index,
+                      const int32_t* process, const int8_t* type, const int8_t* f, const int64_t* v0,
+                      const int64_t* v1, const int8_t* vflags, int32_t n_ranks, int32_t capacity_log2,
+                      int8_t* out_valid, int64_t* out_fail_idx, int64_t* out_fail_inv, int64_t* out_prev_ok,
+                      int64_t* out_explored, int32_t* out_err, char* err, int32_t err_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -169,7 +169,17 @@ struct lc_plan {
   int8_t* dp_lm = nullptr;
   char* hpack = nullptr;  // pinned staging of d_dpack (kept across calls)
   size_t hpack_bytes = 0;
-  std::vector<std::vector<uint8_t>> widths;  // per history, per step live width (team planner)
+  // per history: how many of its steps have live width L (L = 0..32), for the team planner's
+  // step-time models (a sum over 33 widths instead of over every step)
+  struct WidthHist {
+    uint32_t c[33];
+    uint32_t steps() const {
+      uint32_t s = 0;
+      for (uint32_t x : c) s += x;
+      return s;
+    }
+  };
+  std::vector<WidthHist> widths;
   DevArray d_tany, d_tanyoff, d_tdone;
   DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_tlbits, d_thist;
   struct StepBytes { double lds, hbm; };
@@ -424,7 +434,7 @@ struct lc_plan {
     const int L = 32 - __builtin_clz(live);
     const int H = L > 3 ? L - 3 : 0;
     const int He = __builtin_popcount(live >> 3);
-    const double W = std::ldexp(1.0, H), We = std::ldexp(1.0, He);
+    const double W = (double)(1ull << H), We = (double)(1ull << He);
     StepBytes b{8.0 * We * (2.0 + 0.5 * He) + 12.0 * W, 4.0 * (1 + ninv)};
     const int te = __builtin_popcount(live >> DENSE_LMAX);
     if (te) b.hbm += 8.0 * We * (1.0 + 0.5 * te + 0.5);
@@ -453,6 +463,10 @@ struct lc_plan {
   // Step streams for the dense closure-table kernels (format: dense.hpp). Eligible:
   // cas-register, <= DENSE_MAX_STATES register values, live width <= dense_maxw.
   int build_dense() {
+    const auto t_build = std::chrono::steady_clock::now();
+    auto ms_since_build = [&] {
+      return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build).count();
+    };
     dense_b.clear();
     dense_w.clear();
     dense_x.clear();
@@ -460,7 +474,7 @@ struct lc_plan {
     if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0 || dgrid_m <= 0) return 0;
     const int n = enc.n_hist;
     std::vector<double> cost(n, 0.0);
-    widths.resize(n);  // per step live width (team planner); inner buffers kept across calls
+    widths.resize(n);
     plan_lb.assign(n, 0);
     // sizes first (one header per step plus one word per invocation), then every history's
     // stream filled in parallel into its own range
@@ -502,7 +516,8 @@ struct lc_plan {
       sbeg[h] = wcount[h];
       nst[h] = enc.n_steps(h);
       lm[h] = (int8_t)std::max(1, enc.live_max[h]);
-      widths[h].resize(nst[h]);
+      WidthHist& wh = widths[h];
+      std::fill(wh.c, wh.c + 33, 0u);
       uint32_t* out = words + wcount[h];
       uint32_t live = 0;
       for (int t = 0; t < nst[h]; ++t) {
@@ -520,7 +535,7 @@ struct lc_plan {
         }
         const int L = 32 - __builtin_clz(live);
         cost[h] += (double)(1u << L) * L;
-        widths[h][t] = (uint8_t)L;
+        ++wh.c[L];
         const StepBytes sb = step_alg_bytes(live, (int)(q1 - q0));
         dalg[dalg_off[h] + t] = sb;
         dalg_tot[h].lds += sb.lds, dalg_tot[h].hbm += sb.hbm;
@@ -534,6 +549,7 @@ struct lc_plan {
       for (int h = 0; h < n; h += nt) fill(h);
       for (auto& t : th) t.join();
     }
+    const double t_fill = ms_since_build();
     up_ptr = nullptr;  // (a new layout: upload the team tables again)
     for (int h = 0; h < n; ++h) {
       if (!ok[h]) continue;
@@ -544,6 +560,7 @@ struct lc_plan {
        : lw <= DENSE_LMAX ? dense_b : dense_x).push_back(h);
     }
     plan_teams(widths);
+    const double t_plan = ms_since_build();
     // LC_TEAM_ROT=r: a tile team's slots relabelled so its r lowest slots (the ones live in
     // almost every step) become the top r team bits and the others move down r places. Slot
     // labels are arbitrary (masks are sets), so the answer is unchanged; what changes is which
@@ -560,8 +577,8 @@ struct lc_plan {
         const int lw = enc.live_max[h], lb = team_lbits(h);
         if (team_rot < 0) {  // auto: a batch plan's big-tile teams, or mostly-wide histories
           int wide = 0;
-          for (uint8_t L : widths[h]) wide += L > lb;
-          const bool mostly_wide = 10 * wide >= 4 * (int)widths[h].size();
+          for (int L = lb + 1; L <= 32; ++L) wide += (int)widths[h].c[L];
+          const bool mostly_wide = 10 * wide >= 4 * (int)widths[h].steps();
           if (lb < rot_min_lb || !(batch_plan() || mostly_wide)) continue;
         }
         const int r = team_rot < 0 ? lw - lb : std::min(team_rot, lw - lb);
@@ -591,7 +608,7 @@ struct lc_plan {
     pool_block_us = 0, pool_mid_us = 0, pool_wave_us = 0;  // the BLOCK pool's planned work
     for (int h : dense_b) pool_block_us += est_block_us(widths[h]);
     if (dense_pipe & 128) for (int h : dense_m) pool_mid_us += est_mid_us(widths[h]) / 4.0;
-    if (dense_pipe & 64) for (int h : dense_w) pool_wave_us += 7.9 * (double)widths[h].size() / 16.0;
+    if (dense_pipe & 64) for (int h : dense_w) pool_wave_us += 7.9 * (double)widths[h].steps() / 16.0;
     auto heavy_first = [&](int a, int b) { return cost[a] > cost[b]; };
     std::stable_sort(dense_b.begin(), dense_b.end(), heavy_first);
     std::stable_sort(dense_w.begin(), dense_w.end(), heavy_first);
@@ -603,6 +620,7 @@ struct lc_plan {
         o = std::copy(ids->begin(), ids->end(), o);
     }
     dstream_words = wcount[n];
+    const double t_rot = ms_since_build();
     HIP_TRY(d_dpack.ensure(pack));
     HIP_TRY(hipMemcpyAsync(d_dpack.p, hpack, pack, hipMemcpyHostToDevice, stream));
     char* const dp = (char*)d_dpack.p;
@@ -617,6 +635,9 @@ struct lc_plan {
       dense_word_list(DENSE_WORD_BITS, wl.data());
       if ((rc = upload(d_dwords, wl))) return rc;
     }
+    if (debug() || getenv("LC_PHASES"))
+      fprintf(stderr, "[lincheck] build_dense (ms from its start): sizes+fill %.2f  team plan %.2f  rotation+order %.2f  "
+              "upload issued %.2f\n", t_fill, t_plan, t_rot, ms_since_build());
     HIP_TRY(d_dqueue.ensure(16));
     HIP_TRY(d_dstatus.ensure((size_t)std::max(n, 1) * 4));
     HIP_TRY(d_dfail.ensure((size_t)std::max(n, 1) * 4));
@@ -635,15 +656,17 @@ struct lc_plan {
   //   BLOCK step   4.67 + 0.00266 * 2^(L-3)
   //   team step    1.59 + 0.0043 * 2^(min(L,lb)-3) + (L > lb) * (3.87 + 1.57 * (L - lb))
   //   WAVE step    7.9 (16 histories share a workgroup)
-  static double est_block_us(const std::vector<uint8_t>& ws) {
+  static double est_block_us(const WidthHist& ws) {
     double t = 0;
-    for (uint8_t L : ws) t += 4.67 + 0.00266 * std::ldexp(1.0, std::max(0, (int)L - 3));
+    for (int L = 0; L <= 32; ++L)
+      if (ws.c[L]) t += ws.c[L] * (4.67 + 0.00266 * std::ldexp(1.0, std::max(0, L - 3)));
     return t;
   }
   // MID step (4-wave team, LC_PIPE bit 7)   4.9 + 0.0016 * 2^(L-3)  (r2t LC_DEBUG, C3)
-  static double est_mid_us(const std::vector<uint8_t>& ws) {
+  static double est_mid_us(const WidthHist& ws) {
     double t = 0;
-    for (uint8_t L : ws) t += 4.9 + 0.0016 * std::ldexp(1.0, std::max(0, (int)L - 3));
+    for (int L = 0; L <= 32; ++L)
+      if (ws.c[L]) t += ws.c[L] * (4.9 + 0.0016 * std::ldexp(1.0, std::max(0, L - 3)));
     return t;
   }
   double pool_block_us = 0, pool_mid_us = 0, pool_wave_us = 0;  // the planned pool's work (WG-us)
@@ -671,16 +694,18 @@ struct lc_plan {
   // 8.2-9.5 ms as a chain plan, 9.6-9.9 as a batch plan).
   int batch_hist = 600;  // (r2bh: a 500-key share as a chain plan: slowest rank 11.3 -> 10.9 ms)
   bool batch_plan() const { return enc.n_hist > batch_hist; }
-  double est_team_us(const std::vector<uint8_t>& ws, int lb) const {
+  double est_team_us(const WidthHist& ws, int lb) const {
+    const double k = plan_k16 > 0 ? plan_k16 : batch_plan() ? 0.45 : 1.0;
     double t = 0;
-    for (uint8_t L : ws) {
-      const double k = plan_k16 > 0 ? plan_k16 : batch_plan() ? 0.45 : 1.0;
-      t += 1.59 + 0.0043 * k * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
-      if (L > lb) t += 3.87 + plan_x * (L - lb);
+    for (int L = 0; L <= 32; ++L) {
+      if (!ws.c[L]) continue;
+      double u = 1.59 + 0.0043 * k * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
+      if (L > lb) u += 3.87 + plan_x * (L - lb);
+      t += ws.c[L] * u;
     }
     return t;
   }
-  void plan_teams(const std::vector<std::vector<uint8_t>>& ws) {
+  void plan_teams(const std::vector<WidthHist>& ws) {
     const bool pipe_teams = (dense_pipe & 12) == 12;
     const int maxb = (dense_pipe & DENSE_PIPE_SERIAL_SEGS) ? DENSE_TEAM_MAXB_SERIAL : DENSE_TEAM_MAXB;
     const int cap = std::min(dgrid_b, tile_cap);
@@ -694,7 +719,7 @@ struct lc_plan {
     double pool = 0;
     for (int h : dense_b) in_block[h] = 1, est[h] = est_block_us(ws[h]), pool += est[h];
     if (dense_pipe & 64)  // WAVE histories on the big kernel's waves, 16 per workgroup
-      for (int h : dense_w) pool += 7.9 * (double)ws[h].size() / 16.0;
+      for (int h : dense_w) pool += 7.9 * (double)ws[h].steps() / 16.0;
     if (dense_pipe & 128)  // MID histories on the big kernel's waves, 4 per workgroup
       for (int h : dense_m) pool += est_mid_us(ws[h]) / 4.0;
     std::vector<int> cand(dense_x);

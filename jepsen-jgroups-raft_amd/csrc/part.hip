@@ -24,12 +24,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lincheck.h"
@@ -1529,5 +1531,244 @@ int32_t lc_part_run(lc_part* p, void* stream, int64_t max_steps, int64_t* out4, 
 }
 
 void lc_part_destroy(lc_part* p) { delete p; }
+
+}  // extern "C"
+
+namespace {
+
+// A spin barrier for the rank threads of lc_part_check (a level's phases are tens of
+// microseconds: a futex round trip would be a noticeable share of them). wait() returns the
+// error word as the LAST arriver saw it: every rank wrote its errors before arriving, so all
+// ranks leave with the same value and take the same branch (no rank is left in a barrier).
+struct SpinBarrier {
+  std::atomic<int> count{0};
+  std::atomic<int> gen{0};
+  std::atomic<int>* err = nullptr;
+  int snap = 0;
+  int n = 1;
+  int wait() {
+    const int g = gen.load(std::memory_order_acquire);
+    if (count.fetch_add(1, std::memory_order_acq_rel) == n - 1) {
+      count.store(0, std::memory_order_relaxed);
+      snap = err->load(std::memory_order_acquire);
+      gen.store(g + 1, std::memory_order_release);
+      return snap;
+    }
+    for (int spins = 0; gen.load(std::memory_order_acquire) == g; ++spins)
+      if (spins > 1024) std::this_thread::yield();
+    return snap;
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+/* One history, frontier partitioned over n_ranks ranks held by THIS process (SURVEY §8(e)
+ * axis 2 without a collective library): rank r on device r % (visible devices), one host
+ * thread per rank. Per BFS level the ranks' candidate counts are exchanged in host memory and
+ * every receiver pulls its candidates straight out of each sender's staging segment with peer
+ * copies (hipMemcpyPeerAsync: xGMI between MI355X devices; a plain device copy when two ranks
+ * share a device). Same per-history outputs as lc_check. n_ranks == 1 runs lc_part_run (the
+ * device-resident flow kernel); n_ranks <= 0: one rank per visible device. */
+int32_t lc_part_check(int32_t model_kind, int64_t init_value, int64_t n, const int64_t* index,
+                      const int32_t* process, const int8_t* type, const int8_t* f, const int64_t* v0,
+                      const int64_t* v1, const int8_t* vflags, int32_t n_ranks, int32_t capacity_log2,
+                      int8_t* out_valid, int64_t* out_fail_idx, int64_t* out_fail_inv, int64_t* out_prev_ok,
+                      int64_t* out_explored, int32_t* out_err, char* err, int32_t err_len) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    set_msg(err, err_len, "no HIP device visible (the checker has no CPU fallback)");
+    return LC_E_DEVICE;
+  }
+  const int W = n_ranks <= 0 ? std::min(ndev, PW_MAX) : n_ranks;
+  if (W > PW_MAX) {
+    set_msg(err, err_len, "n_ranks %d > %d", W, PW_MAX);
+    return LC_E_ARG;
+  }
+  auto put = [&](int8_t v, int64_t fi, int64_t fv, int64_t po, int64_t ex, int32_t er) {
+    if (out_valid) *out_valid = v;
+    if (out_fail_idx) *out_fail_idx = fi;
+    if (out_fail_inv) *out_fail_inv = fv;
+    if (out_prev_ok) *out_prev_ok = po;
+    if (out_explored) *out_explored = ex;
+    if (out_err) *out_err = er;
+  };
+  std::vector<std::unique_ptr<lc_part, void (*)(lc_part*)>> plans;
+  std::vector<hipStream_t> streams(W, nullptr);
+  auto cleanup = [&]() {
+    for (int r = 0; r < W; ++r)
+      if (streams[r]) {
+        (void)hipSetDevice(r % ndev);
+        (void)hipStreamSynchronize(streams[r]);
+        (void)hipStreamDestroy(streams[r]);
+        streams[r] = nullptr;
+      }
+  };
+  for (int r = 0; r < W; ++r) {
+    lc_part* p = nullptr;
+    const int rc = lc_part_create(r % ndev, model_kind, init_value, n, index, process, type, f, v0, v1, vflags, r,
+                                  W, capacity_log2, &p, err, err_len);
+    if (rc) {
+      cleanup();
+      return rc;
+    }
+    plans.emplace_back(p, lc_part_destroy);
+    if (hipSetDevice(r % ndev) != hipSuccess ||
+        hipStreamCreateWithFlags(&streams[r], hipStreamNonBlocking) != hipSuccess) {
+      set_msg(err, err_len, "stream creation failed on device %d", r % ndev);
+      cleanup();
+      return LC_E_DEVICE;
+    }
+  }
+  lc_part* const p0 = plans[0].get();
+  if (p0->enc.err[0]) {  // an unsearchable history: :unknown with its code, like lc_check
+    put(LC_UNKNOWN, -1, -1, -1, 0, p0->enc.err[0]);
+    cleanup();
+    return 0;
+  }
+  const int64_t ns = p0->enc.n_steps(0);
+  if (W == 1) {
+    int64_t o4[4], r4[4];
+    int rc = lc_part_run(p0, streams[0], -1, o4, err, err_len);
+    if (rc == LC_H_CAPACITY) {
+      put(LC_UNKNOWN, -1, -1, -1, 0, LC_H_CAPACITY);
+      cleanup();
+      return 0;
+    }
+    if (!rc) rc = lc_part_results(p0, o4[1] >= 0 ? o4[1] : ns - 1, streams[0], r4, err, err_len);
+    cleanup();
+    if (rc) return rc;
+    if (o4[1] >= 0) put(LC_INVALID, r4[1], r4[2], r4[3], o4[3], 0);
+    else put(LC_VALID, -1, -1, -1, o4[3], 0);
+    return 0;
+  }
+  // peer access between every pair of devices the ranks use (xGMI); already-enabled is fine
+  for (int a = 0; a < std::min(W, ndev); ++a)
+    for (int b = 0; b < std::min(W, ndev); ++b) {
+      int can = 0;
+      if (a != b && hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can) {
+        (void)hipSetDevice(a);
+        (void)hipDeviceEnablePeerAccess(b, 0);
+        (void)hipGetLastError();
+      }
+    }
+  // shared state: per-level counts [src][dst], per-step frontier sizes, the first error
+  std::vector<int64_t> counts((size_t)W * W, 0), fsize(W, 0);
+  std::atomic<int> fail_rc{0};
+  std::vector<std::string> msgs(W);
+  SpinBarrier bar;
+  bar.n = W;
+  bar.err = &fail_rc;
+  int64_t fail_t = -1, steps_run = 0;
+  auto rank_main = [&](int r) {
+    lc_part* p = plans[r].get();
+    const int dev = r % ndev;
+    hipStream_t s = streams[r];
+    (void)hipSetDevice(dev);
+    char e[256] = {0};
+    uint64_t* recv = nullptr;
+    size_t recv_cap = 0;
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) fail_rc.store(LC_E_DEVICE);
+    auto note = [&](int rc) {  // first error wins; every rank leaves at the next barrier
+      int z = 0;
+      if (rc && fail_rc.compare_exchange_strong(z, rc)) msgs[r] = e;
+    };
+    for (int64_t t = 0; t < ns; ++t) {
+      if (!fail_rc.load()) note(lc_part_step_begin(p, t, s, e, sizeof e));
+      for (;;) {
+        int64_t* mine = &counts[(size_t)r * W];
+        if (!fail_rc.load()) note(lc_part_expand(p, s, mine, e, sizeof e));
+        if (fail_rc.load()) std::fill(mine, mine + W, 0);
+        if (bar.wait()) break;  // every rank's counts are in (or some rank failed: all leave)
+        int64_t total = 0, n_recv = 0;
+        for (int q = 0; q < W * W; ++q) total += counts[q];
+        if (total == 0) break;  // (every rank reads the same counts: all leave together)
+        for (int src = 0; src < W; ++src) n_recv += counts[(size_t)src * W + r];
+        int rc = 0;
+        if ((size_t)n_recv > recv_cap) {
+          if (recv) (void)hipFree(recv);
+          recv = nullptr;
+          recv_cap = std::max<size_t>((size_t)n_recv * 2, 1 << 16);
+          if (hipMalloc(&recv, recv_cap * sizeof(uint64_t)) != hipSuccess) {
+            snprintf(e, sizeof e, "receive buffer of %zu configs on device %d", recv_cap, dev);
+            rc = LC_E_MEMORY;
+          }
+        }
+        // pull this rank's candidates out of every sender's staging segment for it
+        int64_t off = 0;
+        for (int src = 0; src < W && !rc; ++src) {
+          const int64_t c = counts[(size_t)src * W + r];
+          if (!c) continue;
+          const lc_part* q = plans[src].get();
+          const uint64_t* seg = q->stage + (uint64_t)r * q->seg_cap;
+          const hipError_t he = (src % ndev) == dev
+              ? hipMemcpyAsync(recv + off, seg, (size_t)c * 8, hipMemcpyDeviceToDevice, s)
+              : hipMemcpyPeerAsync(recv + off, dev, seg, src % ndev, (size_t)c * 8, s);
+          if (he != hipSuccess) {
+            snprintf(e, sizeof e, "candidate copy rank %d -> %d: %s", src, r, hipGetErrorString(he));
+            rc = LC_E_DEVICE;
+          }
+          off += c;
+        }
+        if (!rc && hipEventRecord(ev, s) != hipSuccess) rc = LC_E_DEVICE;
+        if (!rc) rc = lc_part_absorb(p, s, recv, n_recv, e, sizeof e);
+        if (!rc && hipEventSynchronize(ev) != hipSuccess) rc = LC_E_DEVICE;  // the copies (not the absorb)
+        note(rc);
+        bar.wait();  // every copy out of every staging segment is done: the next expand may refill them
+      }
+      if (!fail_rc.load()) note(lc_part_step_end(p, s, &fsize[r], e, sizeof e));
+      if (bar.wait()) break;  // every rank's frontier size is in
+      int64_t tot = 0;
+      for (int q = 0; q < W; ++q) tot += fsize[q];
+      if (r == 0) steps_run = t + 1;
+      if (tot == 0) {
+        if (r == 0) fail_t = t;
+        break;
+      }
+    }
+    (void)hipStreamSynchronize(s);
+    if (recv) (void)hipFree(recv);
+    if (ev) (void)hipEventDestroy(ev);
+  };
+  {
+    std::vector<std::thread> th;
+    for (int r = 1; r < W; ++r) th.emplace_back(rank_main, r);
+    rank_main(0);
+    for (auto& x : th) x.join();
+  }
+  const int frc = fail_rc.load();
+  if (frc == LC_H_CAPACITY) {
+    put(LC_UNKNOWN, -1, -1, -1, 0, LC_H_CAPACITY);
+    cleanup();
+    return 0;
+  }
+  if (frc) {
+    std::string m;
+    for (auto& x : msgs)
+      if (!x.empty()) m = x;
+    set_msg(err, err_len, "%s", m.empty() ? "partitioned search failed" : m.c_str());
+    cleanup();
+    return frc;
+  }
+  // explored = the sum of the ranks' set cardinalities; the :index triple from any rank
+  int64_t explored = 0, r4[4] = {0, -1, -1, -1};
+  const int64_t tq = fail_t >= 0 ? fail_t : steps_run - 1;
+  for (int r = 0; r < W; ++r) {
+    int64_t o4[4];
+    const int rc = lc_part_results(plans[r].get(), tq, streams[r], o4, err, err_len);
+    if (rc) {
+      cleanup();
+      return rc;
+    }
+    explored += o4[0];
+    if (r == 0) std::copy(o4, o4 + 4, r4);
+  }
+  cleanup();
+  if (fail_t >= 0) put(LC_INVALID, r4[1], r4[2], r4[3], explored, 0);
+  else put(LC_VALID, -1, -1, -1, explored, 0);
+  return 0;
+}
 
 }  // extern "C"

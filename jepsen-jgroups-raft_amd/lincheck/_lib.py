@@ -19,7 +19,7 @@ EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_release", "lc_ch
            "lc_plan_stats", "lc_plan_destroy", "lc_bounds_plan_create", "lc_bounds_plan_sums",
            "lc_bounds_plan_run", "lc_bounds_plan_destroy", "lc_part_create", "lc_part_info",
            "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
-           "lc_part_step_end", "lc_part_results", "lc_part_run", "lc_part_destroy")
+           "lc_part_step_end", "lc_part_results", "lc_part_run", "lc_part_destroy", "lc_part_check")
 ABI_VERSION = 2
 STATS_N = 31
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
@@ -105,6 +105,9 @@ def load():
     L.lc_part_results.restype = C.c_int32
     L.lc_part_run.argtypes = [P, P, C.c_int64, P, C.c_char_p, C.c_int32]
     L.lc_part_run.restype = C.c_int32
+    L.lc_part_check.argtypes = [C.c_int32, C.c_int64, C.c_int64] + [P] * 7 + [C.c_int32, C.c_int32] + \
+        [P] * 6 + [C.c_char_p, C.c_int32]
+    L.lc_part_check.restype = C.c_int32
     L.lc_part_destroy.argtypes = [P]
     L.lc_part_destroy.restype = None
     if L.lc_abi_version() != ABI_VERSION:
@@ -208,6 +211,24 @@ def failure_configs(hist: int, k: int = 10, with_last=False):
     if with_last:
         return cfgs, pending, [int(x) for x in last[:nout[0]]], int(newest[0])
     return cfgs, pending
+
+
+def part_check(h, hist: int = 0, n_ranks: int = 0, capacity_log2: int = 0):
+    """lc_part_check: history `hist` of h with its frontier partitioned over n_ranks in-process
+    ranks (peer copies between devices). Returns lc_check-shaped scalars."""
+    L = load()
+    b, e = int(h.off[hist]), int(h.off[hist + 1])
+    keep = [np.ascontiguousarray(a[b:e]) for a in
+            (h.index, h.process, h.type, h.f, h.v0, h.v1, h.vflags)]
+    out = {"valid": np.zeros(1, np.int8), "fail_idx": np.zeros(1, np.int64),
+           "fail_inv": np.zeros(1, np.int64), "prev_ok": np.zeros(1, np.int64),
+           "explored": np.zeros(1, np.int64), "err": np.zeros(1, np.int32)}
+    buf = _errbuf()
+    rc = L.lc_part_check(1, 0, e - b, *[_p(a) for a in keep], n_ranks, capacity_log2,
+                         _p(out["valid"]), _p(out["fail_idx"]), _p(out["fail_inv"]), _p(out["prev_ok"]),
+                         _p(out["explored"]), _p(out["err"]), buf, len(buf))
+    _raise(rc, buf, "lc_part_check")
+    return out
 
 
 def counter_bounds(init_value: int, h):

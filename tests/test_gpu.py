@@ -818,6 +818,35 @@ def test_gpu_partitioned_run_stage_retry_and_max_steps(flow, monkeypatch):
     assert levels == (full["levels"] if flow == "0" else 0)
 
 
+def _pc_row(g):
+    return tuple(int(g[k][0]) for k in ("valid", "fail_idx", "fail_inv", "prev_ok", "explored"))
+
+
+@pytest.mark.parametrize("ranks", [1, 2, 3, 8])
+def test_gpu_part_check_in_process_ranks_vs_oracle(ranks):
+    """lc_part_check: ONE history, frontier partitioned over in-process ranks (one host thread
+    each, candidates pulled by peer/device copies; a JVM caller's single-call axis 2). On a
+    1-GPU box the ranks share cuda:0. Bit-exact with the oracle for every rank count."""
+    for i, h in enumerate(_part_cases()):
+        g = _lib.part_check(h, n_ranks=ranks)
+        assert int(g["err"][0]) == 0
+        assert _pc_row(g) == _oracle_part_row(h), (ranks, i, g)
+
+
+def test_gpu_part_check_c2_full_two_ranks_and_capacity():
+    """C2 at full size over 2 in-process ranks (22,736 BFS levels through the host exchange):
+    the dense path's verdict and explored count; a capacity too small for the frontier gives
+    :unknown with LC_H_CAPACITY on every rank count."""
+    h = synth.gen_config("c2")
+    g = _lib.part_check(h, n_ranks=2)
+    d = _lib.check(1, 0, h)
+    assert (int(g["valid"][0]), int(g["explored"][0])) == (int(d["valid"][0]), int(d["explored"][0]))
+    small = synth.gen_config("c2", scale=0.1)
+    for ranks in (1, 2):
+        g = _lib.part_check(small, n_ranks=ranks, capacity_log2=10)
+        assert int(g["valid"][0]) == 2 and int(g["err"][0]) == -7
+
+
 def _gpu_part_worker(rank, world, port, q):
     import torch.distributed as tdist
     from lincheck import partition
