@@ -66,18 +66,21 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = Fals
     import oracle  # noqa: E402  (bench cpu_baseline leg only)
     n = h.n_hist
     if n > 1:
-        sample = list(range(n)) if full else list(range(0, n, 20))
+        stride = max(1, n // 50)
+        sample = list(range(n)) if full else list(range(0, n, stride))
         hs = h.select(sample)
         t0 = time.perf_counter()
         res = oracle.check_many(model, hs, n_threads=threads)
         wall = time.perf_counter() - t0
         per = np.array([r["wall_ns"] for r in res], np.float64) / 1e9
-        desc = (f"all {n} keys" if full else f"every 20th key ({len(sample)} of {n}: 0, 20, ...)") + \
+        desc = (f"all {n} keys" if full or stride == 1 else
+                f"every {stride}th key ({len(sample)} of {n}: 0, {stride}, ...)") + \
             f", {threads} threads taking keys from a shared counter"
         used = threads
-        keys = {"min_s": round(float(per.min()), 4), "median_s": round(float(np.median(per)), 4),
-                "max_s": round(float(per.max()), 3), "sum_s": round(float(per.sum()), 3),
-                "slowest_key": int(sample[int(per.argmax())])}
+        keys = {"min_s": round(float(per.min()), 5), "median_s": round(float(np.median(per)), 5),
+                "max_s": round(float(per.max()), 4), "sum_s": round(float(per.sum()), 4),
+                "slowest_key": int(sample[int(per.argmax())]),
+                "ops_per_s_if_perfectly_packed": ops_of(hs) / max(float(per.sum()) / threads, 1e-9)}
     else:
         # one history: the oracle is single-threaded like Knossos's per-history search;
         # time the longest prefix that fits the budget, growing from a short one (a wide
@@ -102,9 +105,12 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = Fals
            "configs_per_s": sum(r["explored"] for r in res) / wall}
     if keys is not None:
         # the sample's wall is max(sum / threads, slowest key): a key's search is one thread
-        keys["ops_per_s_if_perfectly_packed"] = ops / (keys["sum_s"] / threads)
         out["per_key"] = keys
     return out, res, sample, hs
+
+
+def ops_of(h):
+    return h.n_ops()
 
 
 def whole_workload_cpu(path, workload, threads):
