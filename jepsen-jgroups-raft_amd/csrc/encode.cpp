@@ -9,6 +9,7 @@
 #include <unordered_map>
 
 #include "../../include/lincheck.h"
+#include "pool.hpp"
 
 namespace lc {
 namespace {
@@ -329,7 +330,7 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
 }  // namespace
 
 void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
-            const HistArrays& a, Encoded& out) {
+            const HistArrays& a, Encoded& out, const HistSink* sink) {
   out.model = model;
   out.n_hist = n_hist;
   out.init_value = init_value;
@@ -342,21 +343,19 @@ void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
     o.state_val.clear();
   }
   std::vector<OneOut>& parts = parts_tl;
-  static const int nt_max = [] {  // LC_ENC_THREADS: encoder threads (default: the cores, <= 16)
-    const char* e = getenv("LC_ENC_THREADS");
-    const int n = e && atoi(e) > 0 ? atoi(e) : (int)std::thread::hardware_concurrency();
-    return std::max(1, std::min(n, 16));
-  }();
-  int nt = nt_max;
-  if (hist_off[n_hist] - hist_off[0] < 200000) nt = 1;
-  auto run = [&](auto&& fn) {  // fn(h) over every history, nt threads
-    std::vector<std::thread> th;
-    for (int w = 1; w < nt; ++w)
-      th.emplace_back([&, w] { for (int h = w; h < n_hist; h += nt) fn(h); });
-    for (int h = 0; h < n_hist; h += nt) fn(h);
-    for (auto& t : th) t.join();
+  // the process's worker pool (pool.hpp): its threads persist, so their scratch stays warm
+  const int nt = hist_off[n_hist] - hist_off[0] < 200000 ? 1 : 16;
+  auto run = [&](auto&& fn) {  // fn(h) over every history
+    Pool::get().run(n_hist, nt, std::function<void(int)>(fn));
   };
-  run([&](int h) { encode_one(model, a, hist_off[h], hist_off[h + 1], parts[h]); });
+  run([&](int h) {
+    OneOut& o = parts[h];
+    encode_one(model, a, hist_off[h], hist_off[h + 1], o);
+    if (sink)
+      (*sink)(h, HistView{o.err, o.live_max, o.n_states, o.err ? 0 : (int64_t)o.step_slot.size(),
+                          o.step_slot.data(), o.step_ninv.data(), o.inv_slot.data(), o.inv_a.data(),
+                          o.inv_b.data()});
+  });
 
   // concatenate: offsets first, then every history's part copied in parallel
   out.step_off.assign(n_hist + 1, 0);

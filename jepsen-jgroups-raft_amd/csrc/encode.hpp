@@ -11,6 +11,7 @@
 // reused after a return; a crashed op keeps its slot forever.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -86,9 +87,25 @@ struct Encoded {
   int32_t n_steps(int h) const { return step_off[h + 1] - step_off[h]; }
 };
 
+// One encoded history as encode() has just built it (valid during the sink call only):
+// RETURN steps (returning slot, invocations since the previous step) and the invocations'
+// slots and register operands, in step order.
+struct HistView {
+  int32_t err, live_max, n_states;
+  int64_t n_steps;
+  const uint8_t* step_slot;
+  const int64_t* step_ninv;
+  const uint8_t* inv_slot;
+  const int64_t* inv_a;
+  const int64_t* inv_b;
+};
+// Called by the worker that encoded history h, right after it (its data still in cache).
+using HistSink = std::function<void(int, const HistView&)>;
+
 // model: 1 cas-register, 2 counter. Never throws; per-history problems land in err/errmsg.
-// `out` may be reused across calls (its buffers keep their capacity).
+// `out` may be reused across calls (its buffers keep their capacity). `sink` (optional) sees
+// every history as soon as it is encoded (lc_plan builds its dense step streams there).
 void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
-            const HistArrays& a, Encoded& out);
+            const HistArrays& a, Encoded& out, const HistSink* sink = nullptr);
 
 }  // namespace lc

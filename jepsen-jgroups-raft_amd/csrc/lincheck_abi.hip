@@ -25,6 +25,7 @@
 #include "dense.hpp"
 #include "encode.hpp"
 #include "keys.hpp"
+#include "pool.hpp"
 #include "search.hpp"
 
 namespace lc {
@@ -183,8 +184,6 @@ struct lc_plan {
   DevArray d_tany, d_tanyoff, d_tdone;
   DevArray d_dstamps, d_dlhist, d_tstamps, d_mirror, d_tflags, d_ctl, d_abort, d_wgteam, d_tbase, d_tbits, d_tlbits, d_thist;
   struct StepBytes { double lds, hbm; };
-  std::vector<StepBytes> dalg;     // per dense step: algorithmic bytes
-  std::vector<int64_t> dalg_off;    // [n_hist + 1] first step of each history in dalg
   std::vector<StepBytes> dalg_tot;  // [n_hist] every step's (a history that passes runs them all)
   // team layout last uploaded by run_dense (one launch): unchanged across runs of a plan
   std::vector<int32_t> up_wgteam, up_base, up_hist, up_anyoff;
@@ -311,12 +310,23 @@ struct lc_plan {
       static struct { bool ok; int nwg, db, dw, dm, knwg; } cache[64][3];
       auto& c = cache[device & 63][model & 3];
       if (!c.ok) {
+        // (LC_PHASES: the first query of a kernel loads the library's code object onto the
+        // device, once per process; each query is timed so the one-time cost is attributed)
+        const double t_ev = ms_since(t0);
+        auto t1 = std::chrono::steady_clock::now();
         c.nwg = search_grid_size(model);
+        const double t_search = ms_since(t1);
+        t1 = std::chrono::steady_clock::now();
         c.db = dense_grid_size(DENSE_BIG);
         c.dw = dense_grid_size(DENSE_WAVE);
         c.dm = dense_grid_size(DENSE_MID);
+        const double t_dense = ms_since(t1);
+        t1 = std::chrono::steady_clock::now();
         c.knwg = keys_grid_size(model);
         c.ok = c.nwg > 0 && c.knwg > 0;
+        if (debug() || getenv("LC_PHASES"))
+          fprintf(stderr, "[lincheck] first use of device %d: streams+events %.2f ms, occupancy queries: search %.2f "
+                  "dense %.2f keys %.2f ms\n", device, t_ev, t_search, t_dense, ms_since(t1));
       }
       nwg = c.nwg, dgrid_b = c.db, dgrid_w = c.dw, dgrid_m = c.dm, knwg = c.knwg;
     }
@@ -442,10 +452,17 @@ struct lc_plan {
   }
   // bytes of the steps history h ran (all of them, or up to its failing step)
   StepBytes dense_hist_bytes(int h, int fail_t) const {
-    if (fail_t < 0 && h < (int)dalg_tot.size()) return dalg_tot[h];
-    StepBytes b{0, 0};
-    const int64_t e = fail_t >= 0 ? std::min(dalg_off[h] + fail_t + 1, dalg_off[h + 1]) : dalg_off[h + 1];
-    for (int64_t i = dalg_off[h]; i < e; ++i) b.lds += dalg[i].lds, b.hbm += dalg[i].hbm;
+    if (fail_t < 0) return dalg_tot[h];
+    StepBytes b{0, 0};  // a failing history: its steps up to fail_t, from its stream (in hpack)
+    const uint32_t* w = (const uint32_t*)hpack + ((const int64_t*)(hpack + o_sbeg))[h];
+    const uint32_t* const e = w + dense_nw[h];
+    for (int t = 0; w < e && t <= fail_t; ++t) {
+      const uint32_t hdr = *w++;
+      int ninv = 0;
+      while (w < e && (*w & DENSE_OPW)) ++w, ++ninv;
+      const StepBytes sb = step_alg_bytes(hdr & DENSE_LIVE_MASK, ninv);
+      b.lds += sb.lds, b.hbm += sb.hbm;
+    }
     return b;
   }
 
@@ -462,93 +479,109 @@ struct lc_plan {
 
   // Step streams for the dense closure-table kernels (format: dense.hpp). Eligible:
   // cas-register, <= DENSE_MAX_STATES register values, live width <= dense_maxw.
+  // ---- dense step streams, built in three parts around the encoder (plan_build):
+  //   dense_prepare (before encode): the pinned staging layout, per history an upper-bound
+  //     stream range (its entry count: every entry yields at most one word), knobs;
+  //   dense_sink (inside encode, on the worker that just encoded history h, its arrays still in
+  //     cache): eligibility, the step stream words, the width histogram and byte model;
+  //   build_dense (after encode): team classes, planner, rotation, queue order, ONE async H2D.
+  // Eligible: cas-register, <= DENSE_MAX_STATES register values, live width <= dense_maxw,
+  // <= DENSE_MAX_NINV invocations per step.
+  bool dense_on = false;
+  std::vector<char> dense_ok;
+  std::vector<double> dense_cost;
+  std::vector<int64_t> dense_nw;  // words of each history's step stream
+  size_t o_sbeg = 0, o_nst = 0, o_ord = 0, o_lm = 0, pack_bytes = 0;
+  int64_t pack_words = 0;
+  int dense_prepare(int n, const int64_t* hist_off) {
+    dense_b.clear();
+    dense_w.clear();
+    dense_x.clear();
+    dense_m.clear();
+    dense_on = model == LC_MODEL_CAS_REGISTER && path == 0 && dgrid_b > 0 && dgrid_w > 0 && dgrid_m > 0;
+    if (!dense_on) return 0;
+    dense_ok.assign(n, 0);
+    dense_cost.assign(n, 0.0);
+    dense_nw.assign(n, 0);
+    widths.resize(n);
+    dalg_tot.resize(n);
+    plan_lb.assign(n, 0);
+    pack_words = hist_off[n] - hist_off[0];
+    // everything the dense kernels read goes up in ONE async copy from a pinned staging buffer
+    // (kept across calls: no page faults, DMA at full rate): [words | sbeg | nsteps | order | lmax]
+    o_sbeg = ((size_t)pack_words * 4 + 7) & ~(size_t)7;
+    o_nst = o_sbeg + (size_t)n * 8;
+    o_ord = o_nst + (size_t)n * 4;
+    o_lm = o_ord + (size_t)n * 4;
+    pack_bytes = o_lm + (size_t)n + 8;
+    if (hpack_bytes < pack_bytes) {
+      if (hpack) HIP_TRY(hipHostFree(hpack));
+      hpack = nullptr;
+      hpack_bytes = 0;
+      HIP_TRY(hipHostMalloc(&hpack, pack_bytes + pack_bytes / 4, hipHostMallocDefault));
+      hpack_bytes = pack_bytes + pack_bytes / 4;
+    }
+    int64_t* const sbeg = (int64_t*)(hpack + o_sbeg);
+    for (int h = 0; h < n; ++h) sbeg[h] = hist_off[h] - hist_off[0];
+    return 0;
+  }
+  void dense_sink(int h, const HistView& v) {
+    if (!dense_on) return;
+    int32_t* const nst = (int32_t*)(hpack + o_nst);
+    int8_t* const lm = (int8_t*)(hpack + o_lm);
+    dalg_tot[h] = StepBytes{0, 0};
+    nst[h] = 0;
+    lm[h] = 0;
+    bool ok = !v.err && v.n_states <= DENSE_MAX_STATES && v.live_max <= dense_maxw;
+    for (int64_t t = 0; t < v.n_steps && ok; ++t)  // a step's words must fit the decoders' window
+      if (v.step_ninv[t] > DENSE_MAX_NINV) ok = false;
+    dense_ok[h] = ok;
+    if (!ok) return;
+    nst[h] = (int32_t)v.n_steps;
+    lm[h] = (int8_t)std::max(1, v.live_max);
+    WidthHist& wh = widths[h];
+    std::fill(wh.c, wh.c + 33, 0u);
+    uint32_t* out = (uint32_t*)hpack + ((const int64_t*)(hpack + o_sbeg))[h];
+    uint32_t live = 0;
+    int64_t q = 0;
+    double cost = 0;
+    StepBytes tot{0, 0};
+    for (int64_t t = 0; t < v.n_steps; ++t) {
+      if (t > 0) live &= ~(1u << v.step_slot[t - 1]);
+      const int64_t q1 = q + v.step_ninv[t];
+      for (int64_t k = q; k < q1; ++k) live |= 1u << v.inv_slot[k];
+      const uint32_t j = v.step_slot[t];
+      *out++ = live | (j << DENSE_J_SHIFT);
+      for (int64_t k = q; k < q1; ++k) {
+        const int64_t a = v.inv_a[k], b = v.inv_b[k];
+        const uint32_t am = a == R_ANY ? 0xffu : (a == R_NEVER ? 0u : (1u << a));
+        const uint32_t bm = b < 0 ? 0u : (1u << b);
+        *out++ = (uint32_t)v.inv_slot[k] | (am << 8) | (bm << 16) | DENSE_OPW;
+      }
+      const int L = 32 - __builtin_clz(live);
+      cost += (double)(1u << L) * L;
+      ++wh.c[L];
+      const StepBytes sb = step_alg_bytes(live, (int)(q1 - q));
+      tot.lds += sb.lds, tot.hbm += sb.hbm;
+      q = q1;
+    }
+    dalg_tot[h] = tot;
+    dense_cost[h] = cost;
+    dense_nw[h] = out - ((uint32_t*)hpack + ((const int64_t*)(hpack + o_sbeg))[h]);
+  }
+
   int build_dense() {
     const auto t_build = std::chrono::steady_clock::now();
     auto ms_since_build = [&] {
       return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build).count();
     };
-    dense_b.clear();
-    dense_w.clear();
-    dense_x.clear();
-    dense_m.clear();
-    if (model != LC_MODEL_CAS_REGISTER || path != 0 || dgrid_b <= 0 || dgrid_w <= 0 || dgrid_m <= 0) return 0;
+    if (!dense_on) return 0;
     const int n = enc.n_hist;
-    std::vector<double> cost(n, 0.0);
-    widths.resize(n);
-    plan_lb.assign(n, 0);
-    // sizes first (one header per step plus one word per invocation), then every history's
-    // stream filled in parallel into its own range
-    std::vector<char> ok(n, 0);
-    dalg_off.assign(n + 1, 0);
-    std::vector<int64_t> wcount(n + 1, 0);
-    for (int h = 0; h < n; ++h) {
-      ok[h] = !enc.err[h] && enc.n_states[h] <= DENSE_MAX_STATES && enc.live_max[h] <= dense_maxw;
-      const int64_t s0 = enc.step_off[h], s1 = enc.step_off[h + 1];
-      for (int64_t g = s0; g < s1 && ok[h]; ++g)  // a step's words must fit the decoders' window
-        if (enc.inv_off[g + 1] - enc.inv_off[g] > DENSE_MAX_NINV) ok[h] = 0;
-      dalg_off[h + 1] = dalg_off[h] + (ok[h] ? s1 - s0 : 0);
-      wcount[h + 1] = wcount[h] + (ok[h] ? (s1 - s0) + (enc.inv_off[s1] - enc.inv_off[s0]) : 0);
-    }
-    // everything the dense kernels read goes up in ONE async copy from a pinned staging buffer
-    // (kept across calls: no page faults, DMA at full rate): [words | sbeg | nsteps | order | lmax]
-    const size_t o_sbeg = ((size_t)wcount[n] * 4 + 7) & ~(size_t)7, o_nst = o_sbeg + (size_t)n * 8,
-                 o_ord = o_nst + (size_t)n * 4, o_lm = o_ord + (size_t)n * 4, pack = o_lm + (size_t)n + 8;
-    if (hpack_bytes < pack) {
-      if (hpack) HIP_TRY(hipHostFree(hpack));
-      hpack = nullptr;
-      hpack_bytes = 0;
-      HIP_TRY(hipHostMalloc(&hpack, pack + pack / 4, hipHostMallocDefault));
-      hpack_bytes = pack + pack / 4;
-    }
+    std::vector<char>& ok = dense_ok;
+    std::vector<double>& cost = dense_cost;
     uint32_t* const words = (uint32_t*)hpack;
     int64_t* const sbeg = (int64_t*)(hpack + o_sbeg);
-    int32_t* const nst = (int32_t*)(hpack + o_nst);
     int32_t* const ordp = (int32_t*)(hpack + o_ord);
-    int8_t* const lm = (int8_t*)(hpack + o_lm);
-    std::fill(sbeg, sbeg + n, 0);
-    std::fill(nst, nst + n, 0);
-    std::fill(lm, lm + n, 0);
-    dalg.resize(dalg_off[n]);
-    dalg_tot.resize(n);
-    auto fill = [&](int h) {
-      dalg_tot[h] = StepBytes{0, 0};
-      if (!ok[h]) return;
-      sbeg[h] = wcount[h];
-      nst[h] = enc.n_steps(h);
-      lm[h] = (int8_t)std::max(1, enc.live_max[h]);
-      WidthHist& wh = widths[h];
-      std::fill(wh.c, wh.c + 33, 0u);
-      uint32_t* out = words + wcount[h];
-      uint32_t live = 0;
-      for (int t = 0; t < nst[h]; ++t) {
-        const int64_t g = (int64_t)enc.step_off[h] + t;
-        if (t > 0) live &= ~(1u << enc.step_slot[g - 1]);
-        const int64_t q0 = enc.inv_off[g], q1 = enc.inv_off[g + 1];
-        for (int64_t q = q0; q < q1; ++q) live |= 1u << enc.inv_slot[q];
-        const uint32_t j = enc.step_slot[g];
-        *out++ = live | (j << DENSE_J_SHIFT);
-        for (int64_t q = q0; q < q1; ++q) {
-          const int64_t a = enc.inv_a[q], b = enc.inv_b[q];
-          const uint32_t am = a == R_ANY ? 0xffu : (a == R_NEVER ? 0u : (1u << a));
-          const uint32_t bm = b < 0 ? 0u : (1u << b);
-          *out++ = (uint32_t)enc.inv_slot[q] | (am << 8) | (bm << 16) | DENSE_OPW;
-        }
-        const int L = 32 - __builtin_clz(live);
-        cost[h] += (double)(1u << L) * L;
-        ++wh.c[L];
-        const StepBytes sb = step_alg_bytes(live, (int)(q1 - q0));
-        dalg[dalg_off[h] + t] = sb;
-        dalg_tot[h].lds += sb.lds, dalg_tot[h].hbm += sb.hbm;
-      }
-    };
-    {
-      const int nt = wcount[n] > 200000 ? (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
-      std::vector<std::thread> th;
-      for (int w = 1; w < nt; ++w)
-        th.emplace_back([&, w] { for (int h = w; h < n; h += nt) fill(h); });
-      for (int h = 0; h < n; h += nt) fill(h);
-      for (auto& t : th) t.join();
-    }
     const double t_fill = ms_since_build();
     up_ptr = nullptr;  // (a new layout: upload the team tables again)
     for (int h = 0; h < n; ++h) {
@@ -592,7 +625,7 @@ struct lc_plan {
                     : k < keep + r    ? (uint32_t)(lw - r + (k - keep))
                                       : (uint32_t)(k - r);
         uint32_t* w = words + sbeg[h];
-        uint32_t* const e = words + wcount[h + 1];
+        uint32_t* const e = w + dense_nw[h];
         while (w < e) {
           const uint32_t x = *w;
           if (x & DENSE_OPW) {
@@ -619,10 +652,10 @@ struct lc_plan {
       for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
         o = std::copy(ids->begin(), ids->end(), o);
     }
-    dstream_words = wcount[n];
+    dstream_words = pack_words;
     const double t_rot = ms_since_build();
-    HIP_TRY(d_dpack.ensure(pack));
-    HIP_TRY(hipMemcpyAsync(d_dpack.p, hpack, pack, hipMemcpyHostToDevice, stream));
+    HIP_TRY(d_dpack.ensure(pack_bytes));
+    HIP_TRY(hipMemcpyAsync(d_dpack.p, hpack, pack_bytes, hipMemcpyHostToDevice, stream));
     char* const dp = (char*)d_dpack.p;
     dp_stream = (uint32_t*)dp;
     dp_sbeg = (int64_t*)(dp + o_sbeg);
@@ -636,7 +669,7 @@ struct lc_plan {
       if ((rc = upload(d_dwords, wl))) return rc;
     }
     if (debug() || getenv("LC_PHASES"))
-      fprintf(stderr, "[lincheck] build_dense (ms from its start): sizes+fill %.2f  team plan %.2f  rotation+order %.2f  "
+      fprintf(stderr, "[lincheck] build_dense (ms from its start; streams built in encode): classes %.2f  team plan %.2f  rotation+order %.2f  "
               "upload issued %.2f\n", t_fill, t_plan, t_rot, ms_since_build());
     HIP_TRY(d_dqueue.ensure(16));
     HIP_TRY(d_dstatus.ensure((size_t)std::max(n, 1) * 4));
@@ -1572,10 +1605,15 @@ int plan_build(int device, int model, int64_t init_value, int n_hist, const int6
   p->max_configs = max_configs;
   p->max_t = INT32_MAX;
   std::fill(p->phase_ms, p->phase_ms + 5, 0.0);
-  auto t = clk::now();
-  encode(model, init_value, n_hist, hist_off, a, p->enc);
-  p->phase_ms[0] = ms_since(t);
   int rc = p->init_device();  // records phase_ms[1] (hipSetDevice) and [2] (streams, occupancy)
+  auto t = clk::now();
+  // the dense step streams are written by the encoder's workers as each history is encoded
+  if (!rc) rc = p->dense_prepare(n_hist, hist_off);
+  if (!rc) {
+    const HistSink sink = [p](int h, const HistView& v) { p->dense_sink(h, v); };
+    encode(model, init_value, n_hist, hist_off, a, p->enc, p->dense_on ? &sink : nullptr);
+  }
+  p->phase_ms[0] = ms_since(t);
   t = clk::now();
   if (!rc) rc = p->upload_encoded();  // records phase_ms[4] (build_dense)
   p->phase_ms[3] = ms_since(t) - p->phase_ms[4];
