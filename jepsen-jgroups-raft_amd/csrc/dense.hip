@@ -569,6 +569,7 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
 // per-step schedule with lane shuffles for the pulls: no LDS round trip on a word's chain (C1's
 // histories are 5..7 slots wide: ~16 words, a few shuffles per layer).
 constexpr int PIPE_REG = 1024;
+constexpr int PIPE_REG_FIX = 2048;  // REG histories: the closure as a whole-table fixpoint
 constexpr int REG_LMAX = 9;
 
 // close_in_word with the in-word ops and the returning op's passed by value (no indexed array)
@@ -636,7 +637,47 @@ __device__ __forceinline__ void run_regs(const DenseParams& p, int h, OpSel* opt
     const uint32_t pm = (w & jh) ? jh : w;  // bits this word pulls over (only j when it holds j)
     const bool valid = w < (1u << H) && !(w & ~(live >> 3));
     const int pc = __popc(w);
-    for (int q = 0; q <= H; ++q) {
+    if (p.pipe & PIPE_REG_FIX) {
+      // ---- the closure as a fixpoint over the whole table at once (LC_PIPE bit 11): every word
+      // recomputes what its predecessors produce (hi pulls by lane shuffles, the low ops inside
+      // the word) from the current table until no word changes. The layer DP above visits the
+      // H + 1 popcount layers in order, each a dependent chain of up to 8 low-op transfers;
+      // here an iteration's transfers are independent, and a step needs as many iterations as
+      // its longest chain of linearizations (+1 to see no change). Same least fixpoint, so the
+      // same produced set R and explored count.
+      const bool j_lo = j < 3;
+      const uint64_t notj64 = j_lo ? keep64(j) : ~0ull;
+      const uint32_t notj = j_lo ? keep8(j) : 0xffu;
+      const uint32_t lo_ops = live & 7u & ~(j_lo ? (1u << j) : 0u);
+      const bool holds_j = (w & jh) != 0;
+      const OpSel olo[3] = {o0, o1, o2};
+      const uint64_t X = valid ? Bw : 0ull;
+      uint64_t R = 0;
+      for (int it = 0; it <= L + 1; ++it) {
+        const uint64_t B = X | R;
+        uint64_t Rn = 0;
+#pragma unroll
+        for (int b = 0; b < REG_LMAX - 3; ++b) {
+          if (b >= H) break;
+          const uint64_t v = (uint64_t)__shfl_xor((unsigned long long)B, 1 << b, 64) & notj64;
+          if ((pm >> b) & 1u) Rn |= transfer(oh[b], (foldm >> (b + 3)) & 1u, v);
+        }
+        if (!holds_j) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+            if (lo_ops & (1u << k))
+              Rn |= transfer_lo(olo[k], (foldm >> k) & 1u, B, keep8(k) & notj, keep64(k) & notj64, 1 << k);
+          if (j_lo) Rn |= transfer_lo(olo[j], (foldm >> j) & 1u, B, notj, notj64, 1 << j);
+        }
+        Rn = valid ? Rn : 0ull;
+        const bool grew = __any(Rn != R);  // (R only grows)
+        R = Rn;
+        if (!grew) break;
+      }
+      expl += (uint32_t)__popcll(R);
+      Bw = X | R;
+    }
+    for (int q = 0; q <= H && !(p.pipe & PIPE_REG_FIX); ++q) {
       uint64_t R = 0;
 #pragma unroll
       for (int b = 0; b < REG_LMAX - 3; ++b) {

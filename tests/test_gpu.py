@@ -470,7 +470,7 @@ def test_gpu_dense_team_planner(plan, monkeypatch):
 
 
 @pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "15", "27", "47", "79", "143", "207",
-                                  "515", "539", "591", "719", "975", "1999"])
+                                  "515", "539", "591", "719", "975", "1999", "3139", "4047"])
 def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     """LC_PIPE bit 0 / bit 1: BLOCK / WAVE teams overlap consecutive RETURN steps (step t+1's
     layer q beside step t's layer q + 2, returns read through the previous step's slot, fresh
@@ -480,7 +480,8 @@ def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     histories on the big kernel's waves, 143/207 MID histories as 4-wave teams inside big
     workgroups (LDS barriers of their own). +512: double-buffered tables (a step after an
     in-word return starts one super-layer after its predecessor). +1024: WAVE histories of at most
-    9 slots in one wave's registers (lane shuffles)."""
+    9 slots in one wave's registers (lane shuffles); +2048: their closure as a whole-table
+    fixpoint instead of the popcount-layer DP."""
     monkeypatch.setenv("LC_PIPE", pipe)
     hs = [synth.gen_register_keys(24, 600, 5, 0.01, config_id=3, invalid_keys=(1, 7, 16))]
     hs += [synth.gen_register(120, 5, 0.1, 33000 + t, invalid=(t % 2 == 1)) for t in range(8)]
@@ -532,7 +533,7 @@ def _low_slot_rounds(n_rounds, seed, perturb=False):
     return H.encode(ops)
 
 
-@pytest.mark.parametrize("pipe", ["0", "11", "207", "719", "975", "1999"])
+@pytest.mark.parametrize("pipe", ["0", "11", "207", "719", "975", "1999", "4047"])
 def test_gpu_dense_low_slot_orderings(pipe, monkeypatch):
     """The in-word closure's op sequence (0 1 2 0 1 0 2 for three live low ops, a b a for two):
     RETURNs of slot 3 with slots 0..2 pending, writes among them; bit-exact with the oracle,
