@@ -51,6 +51,8 @@
               :else       (do (aset vflags i (byte 1)) (aset v0 i (long v))))))
     {:off off :index index :process process :types types :fs fs :v0 v0 :v1 v1 :vflags vflags}))
 
+(defn- client-ops [history] (filterv #(integer? (:process %)) history))
+
 (defn- failure-configs
   "lc_failure_configs (ABI 2) for history i of the lc_check this thread just made: up to k
   pre-failure configs as {:model {:value v} :linearized [inv-index ...] :last-op ok-index
@@ -158,6 +160,30 @@
                                            (final-paths (:model opts) configs (aget finv i) ops 10)))
                     r)))))))))
 
+(defn check-partitioned
+  "ONE history with its frontier partitioned over n-ranks ranks of this process (lc_part_check:
+  rank r on device r mod visible devices, candidates moved by peer copies over xGMI): for a
+  history whose frontier outgrows one GPU (SURVEY §8(e) axis 2, e.g. the counter path's whole
+  history at counter.clj:133-137 when registered as a cas-register). Same map as
+  check-histories gives, without the failure report."
+  [history n-ranks]
+  (let [ops   (client-ops history)
+        {:keys [off index process types fs v0 v1 vflags]} (encode [ops])
+        valid (byte-array 1) fail (long-array 1) finv (long-array 1) prev (long-array 1)
+        explored (long-array 1) errs (int-array 1) err (byte-array 512)
+        rc    (.invokeInt (lib-fn "lc_part_check")
+                          (object-array [(int 1) (long 0) (long (count ops)) index process types fs
+                                         v0 v1 vflags (int n-ranks) (int 0) valid fail finv prev
+                                         explored errs err (int 512)]))]
+    (when-not (zero? rc)
+      (throw (ex-info (c-string err) {:rc rc})))
+    (let [at (fn [idx] (first (filter #(= idx (:index %)) ops)))
+          v  (aget valid 0)]
+      (cond-> {:valid? (case v 1 true 0 false :unknown) :analyzer :linear :explored (aget explored 0)}
+        (= 2 v)   (assoc :error (get err-text (aget errs 0) "undecided"))
+        (zero? v) (assoc :op (at (aget fail 0)) :previous-ok (at (aget prev 0))
+                         :last-op (at (aget prev 0)))))))
+
 (defn- model-kind
   "[model_kind init] for the models the GPU implements, else nil (-> Knossos)."
   [m]
@@ -165,7 +191,6 @@
         (= "CounterModel" (.getSimpleName (class m)))       [2 (long (:value m))]
         :else nil))
 
-(defn- client-ops [history] (filterv #(integer? (:process %)) history))
 
 (defn linearizable
   "Same options as checker/linearizable. Models the GPU does not implement (the election

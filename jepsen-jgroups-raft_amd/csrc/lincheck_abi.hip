@@ -506,7 +506,10 @@ struct lc_plan {
     widths.resize(n);
     dalg_tot.resize(n);
     plan_lb.assign(n, 0);
-    pack_words = hist_off[n] - hist_off[0];
+    // history h's range: its entry count + 1 words (every entry yields at most one word; the +1
+    // holds the terminator the decoders need: a step's op words are counted up to the first word
+    // without DENSE_OPW, which must not be a neighbour's stale word)
+    pack_words = hist_off[n] - hist_off[0] + n;
     // everything the dense kernels read goes up in ONE async copy from a pinned staging buffer
     // (kept across calls: no page faults, DMA at full rate): [words | sbeg | nsteps | order | lmax]
     o_sbeg = ((size_t)pack_words * 4 + 7) & ~(size_t)7;
@@ -522,7 +525,7 @@ struct lc_plan {
       hpack_bytes = pack_bytes + pack_bytes / 4;
     }
     int64_t* const sbeg = (int64_t*)(hpack + o_sbeg);
-    for (int h = 0; h < n; ++h) sbeg[h] = hist_off[h] - hist_off[0];
+    for (int h = 0; h < n; ++h) sbeg[h] = hist_off[h] - hist_off[0] + h;
     return 0;
   }
   void dense_sink(int h, const HistView& v) {
@@ -568,6 +571,7 @@ struct lc_plan {
     dalg_tot[h] = tot;
     dense_cost[h] = cost;
     dense_nw[h] = out - ((uint32_t*)hpack + ((const int64_t*)(hpack + o_sbeg))[h]);
+    *out = 0u;  // the terminator (no DENSE_OPW): the last step's op words end here
   }
 
   int build_dense() {
