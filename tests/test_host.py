@@ -218,6 +218,75 @@ def test_shard_histories_lpt(n_shards):
         assert np.all(a == 0)
 
 
+def _live_widths_lff(h, k):
+    """Per RETURN step, the live width of history k's table (lowest-free-first slots, crashed ops
+    keep theirs): the encoder's slot policy never widens a table beyond it."""
+    a, b = int(h.off[k]), int(h.off[k + 1])
+    status, pend = {}, {}
+    for i in range(a, b):
+        p = int(h.process[i])
+        if h.type[i] == 0:
+            pend[p] = i
+        else:
+            status[pend.pop(p)] = int(h.type[i])
+    used, slot, out = set(), {}, []
+    pend = {}
+    for i in range(a, b):
+        p = int(h.process[i])
+        if h.type[i] == 0:
+            if status.get(i) == 2:  # failed ops never enter the search
+                continue
+            s = 0
+            while s in used:
+                s += 1
+            used.add(s)
+            slot[i] = s
+            pend[p] = i
+        elif h.type[i] == 1:
+            inv = pend.pop(p)
+            out.append(max(used) + 1)
+            used.discard(slot[inv])
+        elif p in pend:
+            pend.pop(p)  # :info: the slot stays taken; :fail completions had no slot
+    return out
+
+
+@pytest.mark.parametrize("n_shards", [1, 2, 8])
+def test_shard_histories_by_cost(n_shards):
+    """lc_shard_histories_by_cost (lc_check(n_gpus > 1) and bench --gpus N): host only. The cost
+    is each history's modeled chain time: for the C3 shape every key has ~2,000 entries, so the
+    entry split is blind to it, while the modeled time follows the live widths (a step's table
+    has 2^width masks). Every history on one shard, deterministic, LPT bound on the costs."""
+    h = synth.gen_register_keys(64, 400, 5, 0.02, config_id=3)
+    a, cost = _lib.shard_histories_by_cost(1, 0, h, n_shards)
+    b, cost2 = _lib.shard_histories_by_cost(1, 0, h, n_shards)
+    assert np.array_equal(a, b) and np.array_equal(cost, cost2)
+    assert a.min() >= 0 and a.max() < n_shards and np.all(cost > 0)
+    load = np.bincount(a, weights=cost, minlength=n_shards)
+    assert load.max() <= cost.sum() / n_shards + cost.max() + 1e-6
+    # the model per class (the team planner's fits, DESIGN §6): a WAVE history (width <= 11, one
+    # wave: 7.9 us per step) costs more per step than a MID one (12..14, four waves: 4.9 us +
+    # 0.0016 * 2^(L-3)), a BLOCK one (15..17) 4.67 + 0.00266 * 2^(L-3); widths as the encoder
+    # gives them, no wider than lowest-free-first
+    seen = set()
+    for k in range(h.n_hist):
+        ws = _live_widths_lff(h, k)
+        n, lw = len(ws), max(ws)
+        if lw <= 11:
+            assert cost[k] == pytest.approx(7.9 * n), k
+            seen.add("wave")
+        elif lw <= 14:
+            assert 4.9 * n <= cost[k] <= (4.9 + 0.0016 * 2 ** 11) * n, k
+            seen.add("mid")
+        elif lw <= 17:
+            assert 4.67 * n <= cost[k] <= (4.67 + 0.00266 * 2 ** 14) * n, k
+    assert seen == {"wave", "mid"}
+    # counter histories balance by entry count
+    c = H.concat([synth.gen_counter(n, 4, 0.0, 70 + n) for n in (50, 200, 100)])
+    _, ccost = _lib.shard_histories_by_cost(2, 0, c, 2)
+    assert list(ccost) == [float(c.off[k + 1] - c.off[k]) for k in range(3)]
+
+
 def test_shard_histories_rejects_bad_args():
     L = _lib.load()
     off = np.array([0, 5, 3], np.int64)  # not monotone
