@@ -570,6 +570,11 @@ __device__ __forceinline__ void history_loop(const DenseParams& p, uint64_t* B, 
 // histories are 5..7 slots wide: ~16 words, a few shuffles per layer).
 constexpr int PIPE_REG = 1024;
 constexpr int PIPE_REG_FIX = 2048;  // REG histories: the closure as a whole-table fixpoint
+// ... for steps at most this wide: a fixpoint iteration costs a fraction of a layer, but a
+// step needs up to L + 1 of them against H + 1 = L - 2 layers (r3c: C1's 5..7-slot histories
+// 0.498 -> 0.379 ms of kernel time with it on every REG step; C3, whose REG keys reach 9 slots,
+// 11.39 -> 11.60 ms)
+constexpr int REG_FIX_MAXL = 7;
 constexpr int REG_LMAX = 9;
 
 // close_in_word with the in-word ops and the returning op's passed by value (no indexed array)
@@ -637,7 +642,8 @@ __device__ __forceinline__ void run_regs(const DenseParams& p, int h, OpSel* opt
     const uint32_t pm = (w & jh) ? jh : w;  // bits this word pulls over (only j when it holds j)
     const bool valid = w < (1u << H) && !(w & ~(live >> 3));
     const int pc = __popc(w);
-    if (p.pipe & PIPE_REG_FIX) {
+    const bool fix = (p.pipe & PIPE_REG_FIX) && L <= REG_FIX_MAXL;
+    if (fix) {
       // ---- the closure as a fixpoint over the whole table at once (LC_PIPE bit 11): every word
       // recomputes what its predecessors produce (hi pulls by lane shuffles, the low ops inside
       // the word) from the current table until no word changes. The layer DP above visits the
@@ -677,7 +683,7 @@ __device__ __forceinline__ void run_regs(const DenseParams& p, int h, OpSel* opt
       expl += (uint32_t)__popcll(R);
       Bw = X | R;
     }
-    for (int q = 0; q <= H && !(p.pipe & PIPE_REG_FIX); ++q) {
+    for (int q = 0; q <= H && !fix; ++q) {
       uint64_t R = 0;
 #pragma unroll
       for (int b = 0; b < REG_LMAX - 3; ++b) {

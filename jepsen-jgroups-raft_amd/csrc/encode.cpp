@@ -348,13 +348,16 @@ void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
   auto run = [&](auto&& fn) {  // fn(h) over every history
     Pool::get().run(n_hist, nt, std::function<void(int)>(fn));
   };
+  thread_local std::vector<char> taken_tl;
+  taken_tl.assign(n_hist, 0);
+  std::vector<char>& taken = taken_tl;
   run([&](int h) {
     OneOut& o = parts[h];
     encode_one(model, a, hist_off[h], hist_off[h + 1], o);
     if (sink)
-      (*sink)(h, HistView{o.err, o.live_max, o.n_states, o.err ? 0 : (int64_t)o.step_slot.size(),
-                          o.step_slot.data(), o.step_ninv.data(), o.inv_slot.data(), o.inv_a.data(),
-                          o.inv_b.data()});
+      taken[h] = (*sink)(h, HistView{o.err, o.live_max, o.n_states, o.err ? 0 : (int64_t)o.step_slot.size(),
+                                     o.step_slot.data(), o.step_ninv.data(), o.inv_slot.data(), o.inv_a.data(),
+                                     o.inv_b.data()});
   });
 
   // concatenate: offsets first, then every history's part copied in parallel
@@ -380,7 +383,7 @@ void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
     out.n_ops[h] = o.n_ops;
     out.step_off[h + 1] = out.step_off[h] + (int32_t)o.step_slot.size();
     out.state_off[h + 1] = out.state_off[h] + (int64_t)o.state_val.size();
-    inv_base[h + 1] = inv_base[h] + (o.err ? 0 : (int64_t)o.inv_slot.size());
+    inv_base[h + 1] = inv_base[h] + (o.err || taken[h] ? 0 : (int64_t)o.inv_slot.size());
   }
   const int64_t ns = out.step_off[n_hist], ni = inv_base[n_hist];
   out.state_val.resize(out.state_off[n_hist]);
@@ -399,14 +402,15 @@ void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
     std::copy(o.state_val.begin(), o.state_val.end(), out.state_val.begin() + out.state_off[h]);
     const int64_t s0 = out.step_off[h];
     int64_t ib = inv_base[h];
+    const bool keep_inv = !o.err && !taken[h];
     for (size_t s = 0; s < o.step_slot.size(); ++s) {
       out.step_slot[s0 + s] = o.step_slot[s];
       out.step_cmp_idx[s0 + s] = o.step_cmp_idx[s];
       out.step_inv_idx[s0 + s] = o.step_inv_idx[s];
-      ib += o.step_ninv[s];
+      if (keep_inv) ib += o.step_ninv[s];
       out.inv_off[s0 + s + 1] = ib;
     }
-    if (!o.err) {
+    if (keep_inv) {
       const int64_t q0 = inv_base[h];
       std::copy(o.inv_slot.begin(), o.inv_slot.end(), out.inv_slot.begin() + q0);
       std::copy(o.inv_kind.begin(), o.inv_kind.end(), out.inv_kind.begin() + q0);

@@ -100,7 +100,10 @@ struct HistView {
   const int64_t* inv_b;
 };
 // Called by the worker that encoded history h, right after it (its data still in cache).
-using HistSink = std::function<void(int, const HistView&)>;
+// Returns true when the caller has taken everything it needs of h's invocations: `out` then
+// keeps h's RETURN steps (slots, :index values) but not its per-invocation arrays (inv_off does
+// not advance over h's steps).
+using HistSink = std::function<bool(int, const HistView&)>;
 
 // model: 1 cas-register, 2 counter. Never throws; per-history problems land in err/errmsg.
 // `out` may be reused across calls (its buffers keep their capacity). `sink` (optional) sees

@@ -528,8 +528,10 @@ struct lc_plan {
     for (int h = 0; h < n; ++h) sbeg[h] = hist_off[h] - hist_off[0] + h;
     return 0;
   }
-  void dense_sink(int h, const HistView& v) {
-    if (!dense_on) return;
+  bool keep_inv_arrays = false;  // lc_failure_configs: its grid re-run needs every history's
+  // returns true when h's step stream was built (its invocation arrays are then not needed)
+  bool dense_sink(int h, const HistView& v) {
+    if (!dense_on) return false;
     int32_t* const nst = (int32_t*)(hpack + o_nst);
     int8_t* const lm = (int8_t*)(hpack + o_lm);
     dalg_tot[h] = StepBytes{0, 0};
@@ -539,7 +541,7 @@ struct lc_plan {
     for (int64_t t = 0; t < v.n_steps && ok; ++t)  // a step's words must fit the decoders' window
       if (v.step_ninv[t] > DENSE_MAX_NINV) ok = false;
     dense_ok[h] = ok;
-    if (!ok) return;
+    if (!ok) return false;
     nst[h] = (int32_t)v.n_steps;
     lm[h] = (int8_t)std::max(1, v.live_max);
     WidthHist& wh = widths[h];
@@ -572,6 +574,7 @@ struct lc_plan {
     dense_cost[h] = cost;
     dense_nw[h] = out - ((uint32_t*)hpack + ((const int64_t*)(hpack + o_sbeg))[h]);
     *out = 0u;  // the terminator (no DENSE_OPW): the last step's op words end here
+    return !keep_inv_arrays;
   }
 
   int build_dense() {
@@ -1597,7 +1600,7 @@ namespace {
 // kept: lc_check's per-device cached plan) or into a new plan.
 int plan_build(int device, int model, int64_t init_value, int n_hist, const int64_t* hist_off,
                const HistArrays& a, int64_t max_configs, lc_plan** out, std::string& msg,
-               lc_plan* reuse = nullptr) {
+               lc_plan* reuse = nullptr, bool keep_inv_arrays = false) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) {
     return std::chrono::duration<double, std::milli>(clk::now() - t).count();
@@ -1608,13 +1611,15 @@ int plan_build(int device, int model, int64_t init_value, int n_hist, const int6
   p->model = model;
   p->max_configs = max_configs;
   p->max_t = INT32_MAX;
+  p->report = false;
+  p->keep_inv_arrays = keep_inv_arrays;
   std::fill(p->phase_ms, p->phase_ms + 5, 0.0);
   int rc = p->init_device();  // records phase_ms[1] (hipSetDevice) and [2] (streams, occupancy)
   auto t = clk::now();
   // the dense step streams are written by the encoder's workers as each history is encoded
   if (!rc) rc = p->dense_prepare(n_hist, hist_off);
   if (!rc) {
-    const HistSink sink = [p](int h, const HistView& v) { p->dense_sink(h, v); };
+    const HistSink sink = [p](int h, const HistView& v) { return p->dense_sink(h, v); };
     encode(model, init_value, n_hist, hist_off, a, p->enc, p->dense_on ? &sink : nullptr);
   }
   p->phase_ms[0] = ms_since(t);
@@ -2050,7 +2055,7 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
   std::lock_guard<std::mutex> lk(device_mutex(0));
   lc_plan* p = nullptr;
   std::string msg;
-  int rc = plan_build(0, L.model, L.init_value, 1, off, a, 0, &p, msg);
+  int rc = plan_build(0, L.model, L.init_value, 1, off, a, 0, &p, msg, nullptr, true);
   if (rc) {
     set_err(err, err_len, "%s", msg.c_str());
     return rc;
