@@ -238,6 +238,8 @@ def bench_partition(args, rank, world, dist, barrier_sync):
     tdist = dist[1] if dist else None
     h = synth.gen_config(args.workload, scale=args.scale)
     local = gpu_index()
+    if args.in_process:
+        return bench_part_check(args, h, world)
     # per-rank lists of 2^cap configs; C4's widest closures need 2^25 on one rank
     cap = args.capacity_log2 or (25 if args.workload == "c4" else 22)
     runs = []
@@ -295,6 +297,40 @@ def bench_partition(args, rank, world, dist, barrier_sync):
                               "(count exchange + all-to-all), see DESIGN.md §6")},
         "cpu_baseline": None,
     }
+
+
+def bench_part_check(args, h, world):
+    """Axis 2 through lc_part_check: ONE history, its frontier partitioned over --in-process N
+    ranks that are threads of this process (rank r on device r mod visible devices; on a 1-GPU
+    box they share it: this measures the in-process exchange, not xGMI)."""
+    n = args.in_process
+    cap = args.capacity_log2 or (25 if args.workload == "c4" else 22)
+    times, g = [], None
+    for i in range(args.warmup + args.steps):
+        t0 = time.perf_counter()
+        g = _lib.part_check(h, n_ranks=n, capacity_log2=cap)
+        if i >= args.warmup:
+            times.append(time.perf_counter() - t0)
+    el = sum(times)
+    return {
+        "metric": "history ops verified/sec (+ configs explored/sec, % HBM roofline)",
+        "value": h.n_ops() * args.steps / el, "unit": "history ops/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (simulated linearizable SUT, SURVEY §8(d) seeds)",
+        "config": {"workload": f"{args.workload}: one register history, frontier partitioned by "
+                               f"config hash over {n} in-process rank(s) (lc_part_check)",
+                   "ops": h.n_ops(), "scale": args.scale,
+                   "parallelism": f"axis 2: {n} rank threads, peer copies; "
+                                  f"{lc_devices()} visible device(s)"},
+        "configs_explored_per_s": int(g["explored"][0]) * args.steps / el,
+        "verdict": {"valid": int(g["valid"][0]), "explored": int(g["explored"][0]),
+                    "err": int(g["err"][0])},
+        "roofline": None, "cpu_baseline": None}
+
+
+def lc_devices():
+    return int(_lib.load().lc_device_count())
 
 
 def cpu_info():
@@ -358,6 +394,8 @@ def main():
     ap.add_argument("--partition", action="store_true",
                     help="axis 2: one history (c2/c4) with its frontier partitioned over ranks")
     ap.add_argument("--capacity-log2", type=int, default=0, help="--partition: per-rank capacity")
+    ap.add_argument("--in-process", type=int, default=0,
+                    help="--partition: N ranks as threads of this process (lc_part_check)")
     ap.add_argument("--level-protocol", action="store_true",
                     help="--partition at 1 GPU: the host-driven level protocol, not lc_part_run")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
