@@ -797,6 +797,30 @@ __device__ __forceinline__ uint64_t pipe_x(const uint64_t* B, uint32_t w, uint32
   return v & keep_lo;
 }
 
+// LC_PIPE bit 12 (double-buffered tables): a step after a hi-slot return starts ONE super-layer
+// after its predecessor, not two. Step t's frontier word X_t(w) = B_{t-1}(w | j) (j = step t-1's
+// returning slot, a hi bit) is a word of popcount q + 1 that step t-1 finishes in the same
+// super-layer as step t's layer q. But step t-1 computes that word as X_{t-1}(w | j) |
+// T_j(B_{t-1}(w)) (configs holding j are only produced by linearizing j last, never expanded),
+// and both parts are ready a super-layer earlier: B_{t-1}(w) has popcount q, and X_{t-1}(w | j)
+// is a read of step t-2's finished table (popcount q + 1, or q + 2 through a hi return of step
+// t-2). So step t computes its X itself from them; the start rule then only needs step t-2 to
+// be 2 (3) super-layers ahead. Same X, so the same tables, explored counts and verdicts.
+constexpr int PIPE_XHI = 4096;
+
+// X_t(w) of a step whose predecessor (ring entry pv, table Bp; its own predecessor's table Bpp)
+// returned hi slot jp: X_{t-1}(w | jp) | T_jp(B_{t-1}(w)). The caller masks fresh masks / slots.
+__device__ __forceinline__ uint64_t pipe_x_hi(const uint64_t* Bpp, const uint64_t* Bp, const PipeStep* pv,
+                                              uint32_t w, int jp) {
+  const uint32_t pf = pv->fresh;
+  uint64_t pk = ~0ull;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (pf & (1u << k)) pk &= keep64(k);
+  const uint64_t xp = pipe_x(Bpp, w | (1u << (jp - 3)), pf >> 3, pv->jp, pk);
+  return xp | transfer(pv->ops[OP_PAD + jp], (pv->foldm >> jp) & 1u, Bp[w]);
+}
+
 template <typename T>
 __device__ __forceinline__ T rdl(T v, int l) {
   return (T)__builtin_amdgcn_readlane((int)v, l);
@@ -849,6 +873,7 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
     const int ns = p.nsteps[h];
     // double-buffered tables (PIPE_DBL) when two fit the team's LDS: step t on tab(t)
     const bool dbl = (p.pipe & PIPE_DBL) && 2 * NW <= CAPW;
+    const bool xhi = dbl && (p.pipe & PIPE_XHI);  // (needs step t-2's table intact: two tables)
     uint64_t* const B2 = dbl ? B + NW : B;
     auto tab = [&](int t) { return (t & 1) ? B2 : B; };
     const int ntab = dbl ? 2 * NW : NW;
@@ -961,7 +986,11 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
             if (fresh & (1u << k)) keep_lo &= keep64(k);
           const OpSel* ops = st->ops + OP_PAD;
           uint64_t* const Bt = tab(t);
-          const uint64_t X = pipe_x(tab(t - 1), w, fresh >> 3, c.y, keep_lo);
+          const uint64_t X = (xhi && c.y >= 3 && t > 0)
+                                 ? ((w & (fresh >> 3)) ? 0ull
+                                                       : pipe_x_hi(tab(t - 2), tab(t - 1), &ring[(t - 1) % RING], w, c.y) &
+                                                             keep_lo)
+                                 : pipe_x(tab(t - 1), w, fresh >> 3, c.y, keep_lo);
           uint64_t R = pull_set(Bt, w, c.x, ops, foldm);
           R = close_in_word(X, w, live, c.x, ops, foldm, R);
           Bt[w] = X | R;
@@ -1001,7 +1030,11 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
           PipeStep* st = &ring[t % RING];
           const OpSel* ops = st->ops + OP_PAD;
           uint64_t* const Bt = tab(t);
-          const uint64_t X = pipe_x(tab(t - 1), w, fresh >> 3, jp, keep_lo);
+          const uint64_t X = (xhi && jp >= 3 && t > 0)
+                                 ? ((w & (fresh >> 3)) ? 0ull
+                                                       : pipe_x_hi(tab(t - 2), tab(t - 1), &ring[(t - 1) % RING], w, jp) &
+                                                             keep_lo)
+                                 : pipe_x(tab(t - 1), w, fresh >> 3, jp, keep_lo);
           uint64_t R = pull_set(Bt, w, j, ops, foldm);
           R = close_in_word(X, w, live, j, ops, foldm, R);
           Bt[w] = X | R;
@@ -1037,7 +1070,10 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
           const uint32_t w = wn;
           if (r + TEAM < nq) wn = words[o + r + TEAM];
           if (w & ~live_hi) continue;
-          const uint64_t X = pipe_x(Bp, w, fresh_hi, jp, keep_lo);
+          const uint64_t X = (xhi && jp >= 3 && t > 0)
+                                 ? ((w & fresh_hi) ? 0ull
+                                                   : pipe_x_hi(tab(t - 2), Bp, &ring[(t - 1) % RING], w, jp) & keep_lo)
+                                 : pipe_x(Bp, w, fresh_hi, jp, keep_lo);
           uint64_t R = pull_set(Bt, w, j, ops, foldm);
           R = close_in_word(X, w, live, j, ops, foldm, R);
           Bt[w] = X | R;
@@ -1051,17 +1087,29 @@ __device__ __forceinline__ void history_pipe(const DenseParams& p, uint64_t* B, 
       mark(1);
       // ---- decode ahead into a slot nobody read in this super-layer
       const int t_dec_old = t_dec;
-      if (t_dec < ns && t_dec - t_ret_old < RING) {
+      // (with xhi a running step reads its predecessor's ring entry: one slot stays reserved)
+      if (t_dec < ns && t_dec - t_ret_old < RING - (xhi ? 1 : 0)) {
         if (decoder) pipe_decode(p, sw, pos, lane, &ring[t_dec % RING], &ring[(t_dec - 1) % RING]);
         ++t_dec;
       }
       // ---- start the next decoded step at s + 1: two super-layers after its predecessor
       // (one if that has a single layer, or returned an in-word slot on double-buffered
-      // tables), or at once if the predecessor retired
+      // tables; with xhi also after a hi return, when the predecessor's predecessor is 2 (3 after
+      // its own hi return) super-layers ahead), or at once if the predecessor retired
       if (t_run < t_dec_old) {
         const int lp = t_run - 1 - t_ret_old;  // the predecessor's lane (< 0: retired)
-        const int gap = (dbl && lp >= 0 && rdl(h1.x, lp) < 3) ? 1 : 2;
-        const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h1.z, lp) + 1);
+        const int lpp = lp - 1;
+        const bool pred_hi = lp >= 0 && rdl(h1.x, lp) >= 3;
+        bool ok;
+        if (lp < 0 || lp < lead) {
+          ok = true;
+        } else if (xhi && pred_hi) {
+          ok = lpp < 0 || lpp < lead || t_run < 2 ||
+               s + 1 - rdl(h1.w, lpp) >= min(rdl(h1.x, lpp) < 3 ? 2 : 3, rdl(h1.z, lpp) + 1);
+        } else {
+          const int gap = (dbl && !pred_hi) ? 1 : 2;
+          ok = s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h1.z, lp) + 1);
+        }
         if (ok) {
           if (tt == 0) ring[t_run % RING].start = s + 1;
           ++t_run;

@@ -470,7 +470,7 @@ def test_gpu_dense_team_planner(plan, monkeypatch):
 
 
 @pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "15", "27", "47", "79", "143", "207",
-                                  "515", "539", "591", "719", "975", "1999", "3139", "4047"])
+                                  "515", "539", "591", "719", "975", "1999", "3139", "4047", "8143"])
 def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     """LC_PIPE bit 0 / bit 1: BLOCK / WAVE teams overlap consecutive RETURN steps (step t+1's
     layer q beside step t's layer q + 2, returns read through the previous step's slot, fresh
@@ -533,7 +533,7 @@ def _low_slot_rounds(n_rounds, seed, perturb=False):
     return H.encode(ops)
 
 
-@pytest.mark.parametrize("pipe", ["0", "11", "207", "719", "975", "1999", "4047"])
+@pytest.mark.parametrize("pipe", ["0", "11", "207", "719", "975", "1999", "4047", "8143"])
 def test_gpu_dense_low_slot_orderings(pipe, monkeypatch):
     """The in-word closure's op sequence (0 1 2 0 1 0 2 for three live low ops, a b a for two):
     RETURNs of slot 3 with slots 0..2 pending, writes among them; bit-exact with the oracle,
