@@ -806,6 +806,11 @@ __device__ __forceinline__ uint64_t pipe_x(const uint64_t* B, uint32_t w, uint32
 // is a read of step t-2's finished table (popcount q + 1, or q + 2 through a hi return of step
 // t-2). So step t computes its X itself from them; the start rule then only needs step t-2 to
 // be 2 (3) super-layers ahead. Same X, so the same tables, explored counts and verdicts.
+// Off by default: measured (r3e, 8-way rank 0 share) it cuts the super-layers of the WAVE /
+// BLOCK / MID teams by 18 / 23 / 16 %, but each super-layer then holds more steps' words and a
+// longer X chain (two dependent LDS reads), and costs 25-30 % more: the pools end 3-10 % later
+// (C3 11.46 -> 11.46 ms, rank shares unchanged within noise). Bit-exact either way (GPU tests
+// run LC_PIPE 8143).
 constexpr int PIPE_XHI = 4096;
 
 // X_t(w) of a step whose predecessor (ring entry pv, table Bp; its own predecessor's table Bpp)
