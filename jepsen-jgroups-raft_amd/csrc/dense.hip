@@ -1337,10 +1337,19 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
 // Dependencies (1) point to tiles with fewer team bits and (2) to the previous step two
 // super-layers back, so the team runs as a skewed pipeline. Every 8 super-layers each tile
 // waits until all tokens are within 8 super-layers of its own, so a mirror slot is reused
-// only after all its readers passed it (MRING = 32 > 16 + the widest step's 15 layers).
+// only after all its readers passed it (MRING = 64 > 16 + the widest step's 15 + 8 super-layers).
 // Failures are decided after the last step: each tile ORs "read a nonzero X in step t"
 // into the team's bit t in HBM; the leader's first missing bit t names step t - 1.
 constexpr int MRING = DENSE_MRING;
+// LC_PIPE bit 13 (PIPE_GLAY): super-layers index a wide step's GLOBAL popcount layers. Tile r
+// runs its local layer q at super-layer start + q + |r| (|r| = its live team bits), so a pull
+// from tile r \ b reads what that tile finished one super-layer earlier: no tile waits inside
+// a super-layer for another tile's same super-layer, a super-layer costs one hand-off instead of
+// a chain of up to T, and a step spans H + T + 1 super-layers. The start rule, the retire rule
+// and the token waits count the T; the previous step's X (tile r | jp) is read at least two
+// super-layers after it was written, as before. Mirror slots: a step's words are read up to
+// H + T super-layers after its start, plus the 16-super-layer credit lag (MRING = 64).
+constexpr int PIPE_GLAY = 8192;
 
 __device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
                                            unsigned long long need, uint64_t t0, long& spins) {
@@ -1395,6 +1404,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   // LC_PIPE bit 8: tagged mirror words (two granules per word, TagTab): readers poll the data,
   // no token waits before a super-layer, no store drain after it (tokens remain for credits)
   const bool tagged = (p.pipe & 256) != 0;
+  const bool glay = (p.pipe & PIPE_GLAY) != 0;
   const int mshift = HSOLO + (tagged ? 1 : 0);
   auto mirror = [&](int r, int t) {
     return p.mirror + (((size_t)(base + r) * MRING + (size_t)(t % MRING)) << mshift);
@@ -1443,7 +1453,11 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
       h2 = *reinterpret_cast<const int4*>(&st->pstart); // pstart, hp
     }
     const bool run_l = dec_l && tl < t_run;
-    const bool fin_l = run_l && h1.w + h1.z < s;
+    const uint32_t lteam_l = h0.x >> lb;
+    // PIPE_GLAY: a wide step's tile r runs local layer q at super-layer start + q + |r|, so it
+    // spans H + T + 1 super-layers (T = its live team bits)
+    const int tb_l = glay ? __popc(lteam_l) : 0;
+    const bool fin_l = run_l && h1.w + h1.z + tb_l < s;
     const uint64_t fin = __ballot(fin_l);
     const int lead = (int)__builtin_ctzll(~fin);
     // retired steps: this tile read a nonzero frontier in step tl => step tl - 1 survived here
@@ -1453,8 +1467,8 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     t_ret += lead;
     if (t_ret >= ns) break;
     // ---- segments of this tile: running steps whose team slots cover the tile
-    const uint32_t lteam_l = h0.x >> lb;
-    const int q_l = s - h1.w;
+    const int dr_l = glay ? __popc((uint32_t)rank & lteam_l) : 0;  // the tile's layer delay
+    const int q_l = s - h1.w - dr_l;
     const bool seg_l = run_l && (rank & ~lteam_l) == 0 && q_l >= 0 && q_l <= h1.z;
     uint32_t nq_l = 0, o_l = 0, mo_l = 0, mp_l = 0;
     uint32_t pm_l = 0;  // team bits b: pull from tile rank ^ b at this super-layer
@@ -1474,8 +1488,11 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         for (;;) {
           bool ok = true;
           for (uint32_t m = pm_l; m && ok; m &= m - 1)
-            ok = poll_until(p, &flags[rank ^ (1 << __builtin_ctz(m))], (unsigned long long)(s + 1), t0, spins);
-          if (ok && xs_l >= 0) ok = poll_until(p, &flags[xs_l], (unsigned long long)(h2.x + q_l + 1), t0, spins);
+            ok = poll_until(p, &flags[rank ^ (1 << __builtin_ctz(m))], (unsigned long long)(glay ? s : s + 1), t0,
+                            spins);
+          // (PIPE_GLAY: tile xs = r | jp ran the previous step's layer q at pstart + q + |r| + 1)
+          if (ok && xs_l >= 0)
+            ok = poll_until(p, &flags[xs_l], (unsigned long long)(h2.x + q_l + (glay ? dr_l + 2 : 1)), t0, spins);
           if (__all(ok)) break;
         }
       }
@@ -1684,7 +1701,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     if (t_run < t_dec_old) {
       const int lp = t_run - 1 - t_ret_old;
       const int gap = (dbl && lp >= 0 && rdl(h1.x, lp) < 3) ? 1 : 2;  // as in history_pipe
-      const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h1.z, lp) + 1);
+      const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h1.z, lp) + rdl(tb_l, lp) + 1);
       if (ok) {
         if (tid == 0) ring[t_run % RING].start = s + 1, ring[t_run % RING].pstart = last_start;
         last_start = s + 1;

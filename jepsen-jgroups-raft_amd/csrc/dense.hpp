@@ -21,7 +21,7 @@ constexpr int DENSE_WIDE_LMAX = 24;  // widest history a tile team holds (<= 2^7
 constexpr int DENSE_MAX_STATES = 8;  // register values (state ids) per history
 constexpr int DENSE_WORD_BITS = 19;  // bits of the sorted word list (a tile's words use <= 14)
 constexpr int DENSE_MAX_NINV = 30;   // invocations per step (a step must fit a 32-word window)
-constexpr int DENSE_MRING = 32;      // mirror slots per tile (pipelined tile teams)
+constexpr int DENSE_MRING = 64;      // mirror slots per tile (pipelined tile teams)
 constexpr int DENSE_TEAM_MAXB = 8;   // team bits of a pipelined tile team (packed segments)
 constexpr int DENSE_TEAM_MAXB_SERIAL = 5;  // ... with serial segments
 constexpr int DENSE_PIPE_SERIAL_SEGS = 32;  // DenseParams.pipe bit 5: one pass per segment

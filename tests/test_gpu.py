@@ -470,7 +470,8 @@ def test_gpu_dense_team_planner(plan, monkeypatch):
 
 
 @pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "15", "27", "47", "79", "143", "207",
-                                  "515", "539", "591", "719", "975", "1999", "3139", "4047", "8143"])
+                                  "515", "539", "591", "719", "975", "1999", "3139", "4047", "8143",
+                                  "12239"])
 def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     """LC_PIPE bit 0 / bit 1: BLOCK / WAVE teams overlap consecutive RETURN steps (step t+1's
     layer q beside step t's layer q + 2, returns read through the previous step's slot, fresh
@@ -635,6 +636,26 @@ def test_gpu_dense_tile_teams_rotated(rot, lbits, pipe, monkeypatch):
     got = p.results()
     for k in range(h.n_hist):
         _cmp(got, exp[k], k, f"rotated {rot} lbits={lbits} w={widths[k]}")
+    p.close()
+
+
+@pytest.mark.parametrize("pipe", ["11983", "12239"], ids=["tokens", "tagged"])
+@pytest.mark.parametrize("rot,lbits", [("0", None), ("0", "15"), ("0", "14"), ("9", None), ("9", "14"), ("2", "15")])
+def test_gpu_dense_tile_teams_global_layers(rot, lbits, pipe, monkeypatch):
+    """LC_PIPE bit 13: a wide step's tile r runs its local layer q at super-layer
+    start + q + |r| (global popcount layers), so cross-tile pulls read the previous super-layer
+    and a step spans H + T + 1 super-layers. Same answers, unrotated and rotated, with tokens
+    (11983) or tagged mirror words (12239), on teams of 2 to 256 tiles."""
+    monkeypatch.setenv("LC_TEAM_ROT", rot)
+    monkeypatch.setenv("LC_PIPE", pipe)
+    if lbits:
+        monkeypatch.setenv("LC_TILE_LBITS", lbits)
+    h, widths, exp = _wide_batch()
+    p = _lib.Plan(1, 0, h)
+    p.run()
+    got = p.results()
+    for k in range(h.n_hist):
+        _cmp(got, exp[k], k, f"global layers rot={rot} lbits={lbits} w={widths[k]}")
     p.close()
 
 
