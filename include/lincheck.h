@@ -17,8 +17,13 @@
  *
  * History encoding (one op per entry, all histories concatenated, hist_off[n_hist+1]):
  *   type  : 0 :invoke, 1 :ok, 2 :fail, 3 :info
- *   f     : 0 :read, 1 :write, 2 :cas, 3 :add, 4 :decr, 5 :add-and-get, 6 :decr-and-get
+ *   f     : 0 :read, 1 :write, 2 :cas, 3 :add, 4 :decr, 5 :add-and-get, 6 :decr-and-get,
+ *           7 :inspect
  *   vflags: 0 nil, 1 scalar (v0), 2 pair [v0 v1]
+ *   LeaderModel (:inspect, leader.clj:63-75): value [leader term] as a pair with v0 = the
+ *           caller's id for the leader (-1 for nil and for "null", which serialize-leader makes
+ *           equal, leader.clj:51-54; ids equal iff the serialized names are) and v1 = the term;
+ *           a nil value is (leader nil, term nil), as destructuring nil gives
  *   index : the op's :index (NULL -> position within its history)
  * Only client ops (integer :process) may be passed; the encoder namespace drops the rest.
  */
@@ -30,9 +35,9 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 2  /* 2: lc_failure_configs gained last_op / out_last_op */
+#define LC_ABI_VERSION 3  /* 2: lc_failure_configs gained last_op / out_last_op; 3: LC_MODEL_LEADER */
 
-enum lc_model { LC_MODEL_CAS_REGISTER = 1, LC_MODEL_COUNTER = 2 };
+enum lc_model { LC_MODEL_CAS_REGISTER = 1, LC_MODEL_COUNTER = 2, LC_MODEL_LEADER = 3 };
 enum lc_valid { LC_INVALID = 0, LC_VALID = 1, LC_UNKNOWN = 2 };
 enum lc_error {
   LC_OK = 0,
@@ -61,8 +66,14 @@ int32_t lc_device_count(void);
 
 /*
  * Check n_hist histories against the model (knossos.linear semantics).
- *   model_kind   : LC_MODEL_CAS_REGISTER (initial value nil; init_value ignored) or
- *                  LC_MODEL_COUNTER (initial value init_value)
+ *   model_kind   : LC_MODEL_CAS_REGISTER (initial value nil; init_value ignored),
+ *                  LC_MODEL_COUNTER (initial value init_value) or LC_MODEL_LEADER (the
+ *                  :election workload's (LeaderModel. {}), leader.clj:63-85: the empty term ->
+ *                  leader map; init_value ignored). A LeaderModel state is the set of
+ *                  (term, leader) pairs of the ops linearized so far; a pair can only conflict
+ *                  with pairs of its own term, so the search tracks the pairs of terms that
+ *                  carry two or more leaders in the history (at most 64 per history, else
+ *                  LC_UNKNOWN with LC_H_CAPACITY)
  *   n_gpus       : shards to spread histories over (<=0: one per visible device; more
  *                  shards than devices are multiplexed); results do not depend on it
  *   max_configs  : per-history cap on |frontier| + |closure| (<=0: device capacity only);
@@ -120,7 +131,8 @@ int32_t lc_shard_histories_by_cost(int32_t model_kind, int64_t init_value, int32
 /*
  * After lc_check reported history `hist` invalid: the frontier just before the failing :ok,
  * the :configs of a Knossos failure report [ext] (compare as a set; at most k are written, in
- * a fixed order). Config i: model value state[i] (register: nil when is_nil[i]); the pending
+ * a fixed order). Config i: model value state[i] (register: nil when is_nil[i]; leader: the
+ * bitmask of its contested (term, leader) pairs, the caller rebuilds the map); the pending
  * ops it has linearized, as invocation :index values, in linearized[i*64 .. i*64+n_lin[i]) (its
  * Knossos :pending = the pending ops NOT listed there); last_op[i] = :index of the :ok
  * completion of the op it linearized last (Knossos's per-config :last-op), -1 for the initial

@@ -2,7 +2,8 @@
   "Drop-in for (checker/linearizable {:model m :algorithm :linear}) backed by
   liblincheck.so (include/lincheck.h) through JNA. Reference call sites replaced:
   src/jepsen/jgroups/workload/register.clj:106-111 (independent/checker over
-  checker/linearizable) and counter.clj:133-137 (model CounterModel, :100-127).
+  checker/linearizable), counter.clj:133-137 (model CounterModel, :100-127) and leader.clj:79-85
+  (model (LeaderModel. {}), :63-75).
 
   UNTESTED ON A JVM: the build container and the GPU box have no JVM, so this file has
   never been loaded. The Python ctypes harness (lincheck/_lib.py, lincheck/checker.py)
@@ -21,7 +22,12 @@
   (.getFunction ^NativeLibrary @lib ^String fname))
 
 (def type-code {:invoke 0 :ok 1 :fail 2 :info 3})
-(def f-code {:read 0 :write 1 :cas 2 :add 3 :decr 4 :add-and-get 5 :decr-and-get 6})
+(def f-code {:read 0 :write 1 :cas 2 :add 3 :decr 4 :add-and-get 5 :decr-and-get 6 :inspect 7})
+
+(defn- leader-name
+  "serialize-leader (leader.clj:51-54): nil -> \"null\"."
+  [x]
+  (if (nil? x) "null" (str x)))
 
 (def ^:private err-text
   {-4 "malformed history" -5 "too many concurrently pending ops"
@@ -35,6 +41,9 @@
   [histories]
   (let [ops    (vec (apply concat histories))
         n      (count ops)
+        ids    (volatile! {"null" -1})  ; :inspect leaders -> ids (lincheck.h: nil = "null" = -1)
+        lid    (fn [x] (let [nm (leader-name x)]
+                         (or (@ids nm) (let [i (dec (count @ids))] (vswap! ids assoc nm i) i))))
         off    (long-array (reductions + 0 (map count histories)))
         index  (long-array n) process (int-array n) types (byte-array n) fs (byte-array n)
         v0     (long-array n) v1 (long-array n) vflags (byte-array n)]
@@ -45,6 +54,10 @@
         (aset types i (byte (type-code (:type op))))
         (aset fs i (byte (f-code (:f op))))
         (cond (nil? v)    (aset vflags i (byte 0))
+              (= :inspect (:f op))  ; [leader term ...] (leader.clj:14-17, :69)
+                          (do (aset vflags i (byte 2))
+                              (aset v0 i (long (lid (nth v 0))))
+                              (aset v1 i (long (nth v 1))))
               (vector? v) (do (aset vflags i (byte 2))
                               (aset v0 i (long (v 0)))
                               (aset v1 i (long (v 1))))
@@ -89,6 +102,26 @@
                    (if (and i (= :ok (:type o))) (assoc-in out [i :value] (:value o)) out)))))
       out)))
 
+(defn- leader-config-models
+  "LeaderModel configs: the device reports each config's contested (term, leader) pairs only,
+  so its model is rebuilt as the search defines it: (LeaderModel. {}) stepped through every op
+  that returned :ok before the failing completion, then the pending ops the config linearized
+  (a consistent map holds one leader per term, so the order does not matter)."
+  [m configs ops fail-idx]
+  (let [folded   (folded-ops ops)
+        returned (loop [os ops, open {}, out []]
+                   (let [o (first os)]
+                     (if (or (nil? o) (= fail-idx (:index o)))
+                       out
+                       (let [p (:process o)]
+                         (if (= :invoke (:type o))
+                           (recur (rest os) (assoc open p (:index o)) out)
+                           (recur (rest os) (dissoc open p)
+                                  (if (and (open p) (= :ok (:type o))) (conj out (open p)) out)))))))]
+    (vec (for [c configs]
+           (assoc c :model (reduce (fn [mm i] (model/step mm (folded i)))
+                                   m (concat returned (sort (:linearized c)))))))))
+
 (defn- final-paths
   ":final-paths: from each pre-failure config, pending ops linearized one after another (each
   step consistent), ending with the failing op's inconsistent step; breadth-first, <= k."
@@ -98,7 +131,10 @@
         pending (sort (:pending (first configs)))]
     (when fop
       (loop [queue (for [c configs]
-                     [(assoc m :value (get-in c [:model :value])) (set (:linearized c))
+                     [(if (satisfies? model/Model (:model c))  ; LeaderModel: the rebuilt record
+                        (:model c)
+                        (assoc m :value (get-in c [:model :value])))
+                      (set (:linearized c))
                       [{:op nil :model (:model c)}]])
              paths []]
         (if (or (empty? queue) (>= (count paths) k))
@@ -144,7 +180,10 @@
                                  :last-op     (at (aget prev i)))
                (and (zero? v) (:configs opts true))
                ((fn [r]
-                  (if-let [{:keys [configs newest-last-op]} (failure-configs i 10)]
+                  (if-let [{:keys [configs newest-last-op]}
+                           (cond-> (failure-configs i 10)
+                             (= 3 model-kind) (update :configs #(leader-config-models (:model opts) % ops
+                                                                                      (aget fail i))))]
                     (cond-> (assoc r
                                    :last-op (at newest-last-op)
                                    ;; Knossos :configs: {:model :last-op :pending}, :pending =
@@ -189,13 +228,14 @@
   [m]
   (cond (and (instance? CASRegister m) (nil? (:value m))) [1 0]  ; (model/cas-register)
         (= "CounterModel" (.getSimpleName (class m)))       [2 (long (:value m))]
+        (and (= "LeaderModel" (.getSimpleName (class m)))     ; (LeaderModel. {}), leader.clj:84
+             (empty? (:state m)))                            [3 0]
         :else nil))
 
 
 (defn linearizable
-  "Same options as checker/linearizable. Models the GPU does not implement (the election
-  workload's LeaderModel, leader.clj:63-85; a cas-register with a non-nil initial value)
-  fall back to Knossos."
+  "Same options as checker/linearizable. Models the GPU does not implement (a cas-register with
+  a non-nil initial value, a LeaderModel that does not start empty) fall back to Knossos."
   [{:keys [model] :as opts}]
   (if-let [[kind init] (model-kind model)]
     (reify checker/Checker

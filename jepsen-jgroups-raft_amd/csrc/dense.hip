@@ -1187,6 +1187,10 @@ __device__ __forceinline__ void flush_stats(const DenseParams& p, unsigned long 
 constexpr int WAVE_WG = 256;
 // pipeline rings: running steps <= (H + 1) / 2, plus one decoded ahead and one retire margin
 constexpr int WAVE_RING = 8, BLOCK_RING = 16;
+// tile teams: steps decoded ahead + in flight. With global layers (PIPE_GLAY) a step spans
+// H + T + 1 super-layers, so at one start per ~1.2-1.8 super-layers 16 entries ran out (r3g:
+// rotated C3 share 1190 -> 1339 super-layers)
+constexpr int TEAM_RING = 32;
 
 // WAVE teams: one history per wave, 4 waves per workgroup, tables of 2^DENSE_WAVE_LMAX masks.
 __global__ void __launch_bounds__(WAVE_WG) dense_wave_kernel(DenseParams p) {
@@ -1367,7 +1371,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
                                           int team, int base, int rank, int G, int h, int lb, int* sAbort,
                                           unsigned long long& expl, unsigned long long& st_fout) {
   constexpr int HSOLO = DENSE_LMAX - 3;
-  constexpr int RING = 16;
+  constexpr int RING = TEAM_RING;
   const int tid = threadIdx.x, lane = tid & 63;
   const bool decoder = tid < 64;
   const uint32_t lmask = (1u << lb) - 1;
@@ -1855,7 +1859,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   __shared__ unsigned sAny;
   __shared__ unsigned long long sRed;
   __shared__ uint64_t sZero;
-  __shared__ PipeStep sRing[BLOCK_RING];
+  __shared__ PipeStep sRing[TEAM_RING > BLOCK_RING ? TEAM_RING : BLOCK_RING];
   __shared__ uint32_t sCum[BINOM_N * BINOM_N];  // sCum[n][k] = sum of C(n, q) for q < k
 
   const int tid = threadIdx.x, lane = tid & 63;

@@ -15,7 +15,7 @@ namespace lc {
 namespace {
 
 enum { T_INVOKE = 0, T_OK = 1, T_FAIL = 2, T_INFO = 3 };
-enum { F_READ = 0, F_WRITE = 1, F_CAS = 2, F_ADD = 3, F_DECR = 4, F_AAG = 5, F_DAG = 6 };
+enum { F_READ = 0, F_WRITE = 1, F_CAS = 2, F_ADD = 3, F_DECR = 4, F_AAG = 5, F_DAG = 6, F_INSPECT = 7 };
 enum { V_NIL = 0, V_SCALAR = 1, V_PAIR = 2 };
 
 struct OneOut {
@@ -83,6 +83,12 @@ const char* operands(int model, const Op& op, Find&& find_id, uint8_t& kind, int
       default:
         return "unknown :f for cas-register";
     }
+  }
+  if (model == LC_MODEL_LEADER) {  // operands set by the contested-pair pass (encode_one)
+    if (op.f != F_INSPECT) return "unknown :f for LeaderModel";
+    if (op.vflags == V_SCALAR) return ":inspect value is not [leader term]";
+    kind = C_LEADER;
+    return nullptr;
   }
   switch (op.f) {
     case F_ADD:
@@ -240,6 +246,75 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
       return fail(LC_H_MODEL, m);
     }
     op.oa = oa, op.ob = ob;
+  }
+  // LeaderModel (leader.clj:63-75): the state is the set of (term, leader) pairs of the
+  // linearized ops, and a step is inconsistent iff the state holds the op's term with another
+  // leader. Only a term that carries two or more leaders in this history can ever conflict: its
+  // pairs ("contested") get state bits in first-appearance order; every other op steps with
+  // a = b = 0 (always consistent; its pair changes no later decision). A nil value is (leader
+  // nil = id -1, term nil).
+  if (model == LC_MODEL_LEADER) {
+    struct Term { int64_t term, first_leader; bool nil, contested; };
+    struct Pair { int64_t term, leader; bool nil; };
+    std::vector<Term> terms;
+    std::unordered_map<int64_t, int32_t> term_at;  // integer term -> terms[]
+    int32_t nil_term = -1;
+    auto key_of = [](const Op& op, int64_t& t, int64_t& l, bool& nil) {
+      nil = op.vflags == V_NIL;
+      t = nil ? 0 : op.v1;
+      l = nil ? -1 : op.v0;
+    };
+    auto find_term = [&](int64_t t, bool nil) -> int32_t {
+      if (nil) return nil_term;
+      auto it = term_at.find(t);
+      return it == term_at.end() ? -1 : it->second;
+    };
+    for (const Op& op : ops) {
+      if (op.status == T_FAIL) continue;
+      int64_t t, l;
+      bool nil;
+      key_of(op, t, l, nil);
+      const int32_t k = find_term(t, nil);
+      if (k < 0) {
+        if (nil) nil_term = (int32_t)terms.size();
+        else term_at.emplace(t, (int32_t)terms.size());
+        terms.push_back(Term{t, l, nil, false});
+      } else if (terms[k].first_leader != l) {
+        terms[k].contested = true;
+      }
+    }
+    std::vector<Pair> pairs;
+    std::vector<int32_t> pair_term;
+    for (Op& op : ops) {
+      if (op.status == T_FAIL) continue;
+      int64_t t, l;
+      bool nil;
+      key_of(op, t, l, nil);
+      const int32_t k = find_term(t, nil);
+      op.oa = op.ob = 0;
+      if (!terms[k].contested) continue;
+      int bit = -1;
+      for (size_t q = 0; q < pairs.size(); ++q)
+        if (pair_term[q] == k && pairs[q].leader == l) bit = (int)q;
+      if (bit < 0) {
+        if ((int)pairs.size() == LEADER_MAX_PAIRS) {
+          o.live_max = 0;
+          return fail(LC_H_CAPACITY, "more than 64 contested (term, leader) pairs");
+        }
+        bit = (int)pairs.size();
+        pairs.push_back(Pair{t, l, nil});
+        pair_term.push_back(k);
+      }
+      op.ob = (int64_t)(1ull << bit);
+    }
+    for (Op& op : ops) {  // a = the op term's other pairs
+      if (op.status == T_FAIL || !op.ob) continue;
+      const int bit = __builtin_ctzll((uint64_t)op.ob);
+      uint64_t a = 0;
+      for (size_t q = 0; q < pairs.size(); ++q)
+        if (pair_term[q] == pair_term[bit] && (int)q != bit) a |= 1ull << q;
+      op.oa = (int64_t)a;
+    }
   }
 
   // ---- RETURN steps with slot assignment (the policy above, else lowest free slot first).

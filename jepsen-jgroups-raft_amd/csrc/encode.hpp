@@ -22,6 +22,11 @@ namespace lc {
 constexpr int64_t R_ANY = -1, R_NEVER = -2, R_KEEP = -1;
 // counter op kind bits: PRE_EQ (state == a), POST_EQ (state +/- d == a), SUB (d subtracted)
 constexpr uint8_t C_PRE_EQ = 1, C_POST_EQ = 2, C_SUB = 4;
+// LeaderModel op (leader.clj:63-75), on the counter's config layout (the state is a function of
+// the linearized set): consistent iff (state & a) == 0, state |= b; a = the other contested pairs
+// of the op's term, b = its own contested pair (both 0 for a term with one leader)
+constexpr uint8_t C_LEADER = 8;
+constexpr int LEADER_MAX_PAIRS = 64;
 constexpr int MAX_SLOTS = 63;
 
 struct HistArrays {
@@ -105,7 +110,7 @@ struct HistView {
 // not advance over h's steps).
 using HistSink = std::function<bool(int, const HistView&)>;
 
-// model: 1 cas-register, 2 counter. Never throws; per-history problems land in err/errmsg.
+// model: 1 cas-register, 2 counter, 3 leader. Never throws; per-history problems land in err/errmsg.
 // `out` may be reused across calls (its buffers keep their capacity). `sink` (optional) sees
 // every history as soon as it is encoded (lc_plan builds its dense step streams there).
 void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,

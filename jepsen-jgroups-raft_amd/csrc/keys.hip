@@ -186,14 +186,19 @@ __global__ void __launch_bounds__(KB) keys_kernel(KeysParams p) {
               const uint8_t kind = sK[k];
               const int64_t a = sA[k], d = sB[k];
               int64_t r;
-              const bool ovf = (kind & 4) ? __builtin_sub_overflow(c.st, d, &r)
-                                          : __builtin_add_overflow(c.st, d, &r);
-              if (ovf) {  // Clojure +/- throw -> checker error -> :unknown
-                sErr = ST_MODEL;
-                continue;
+              if (kind & 8) {  // LeaderModel.step (leader.clj:69-75): a term's other leader -> inconsistent
+                if (c.st & a) continue;
+                r = c.st | d;
+              } else {
+                const bool ovf = (kind & 4) ? __builtin_sub_overflow(c.st, d, &r)
+                                            : __builtin_add_overflow(c.st, d, &r);
+                if (ovf) {  // Clojure +/- throw -> checker error -> :unknown
+                  sErr = ST_MODEL;
+                  continue;
+                }
+                if ((kind & 1) && c.st != a) continue;
+                if ((kind & 2) && r != a) continue;
               }
-              if ((kind & 1) && c.st != a) continue;
-              if ((kind & 2) && r != a) continue;
               ne.key = c.key | (1ull << k);
               ne.st = r;
             }

@@ -406,7 +406,7 @@ struct lc_plan {
     std::vector<int8_t> ksh(n), kbi(n);
     std::vector<double> cost(n);
     for (int h = 0; h < n; ++h) {
-      init[h] = model == LC_MODEL_CAS_REGISTER ? 0 : enc.init_value;
+      init[h] = model == LC_MODEL_COUNTER ? enc.init_value : 0;  // (register: nil; leader: {})
       beg[h] = enc.step_off[h];
       end[h] = enc.step_off[h + 1];
       ksh[h] = (int8_t)enc.live_max[h];
@@ -1341,7 +1341,7 @@ struct lc_plan {
       st0[i] = enc.err[h] ? ST_SKIP : ST_RUNNING;
       beg[i] = enc.step_off[h];
       end[i] = enc.step_off[h + 1];
-      init[i] = model == LC_MODEL_CAS_REGISTER ? 0 : enc.init_value;
+      init[i] = model == LC_MODEL_COUNTER ? enc.init_value : 0;
     }
     HIP_TRY(hipMemcpyAsync(d_status.p, st0.data(), nh * 4, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemcpyAsync(d_bbeg.p, beg.data(), nh * 4, hipMemcpyHostToDevice, stream));
@@ -1656,7 +1656,7 @@ lc_plan* cached_plan(int dev) {
 bool valid_args(int model, int n_hist, const int64_t* hist_off, const int32_t* process,
                 const int8_t* type, const int8_t* f, const int64_t* v0, const int64_t* v1,
                 const int8_t* vflags, char* err, int32_t err_len) {
-  if (model != LC_MODEL_CAS_REGISTER && model != LC_MODEL_COUNTER) {
+  if (model != LC_MODEL_CAS_REGISTER && model != LC_MODEL_COUNTER && model != LC_MODEL_LEADER) {
     set_err(err, err_len, "unknown model kind %d", model);
     return false;
   }
@@ -2130,7 +2130,7 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
       uint64_t key;
       memcpy(&key, buf.data() + i * E, 8);
       int64_t val = 0;
-      if (L.model == LC_MODEL_COUNTER) memcpy(&val, buf.data() + i * E + 8, 8);
+      if (L.model != LC_MODEL_CAS_REGISTER) memcpy(&val, buf.data() + i * E + 8, 8);
       const int tag = (int)((key >> tag_shift) & 63);
       all.push_back({key & ((1ull << tag_shift) - 1), val, (t_fail - 1 - tag) & 63});
     }

@@ -1,6 +1,6 @@
 // search.hip — the just-in-time linearization search (knossos.linear/analysis [ext],
-// SURVEY §8(a) a5) for cas-register (a6) and CounterModel (a7, counter.clj:100-127) as one
-// persistent, cooperative, level-synchronous kernel on gfx950.
+// SURVEY §8(a) a5) for cas-register (a6), CounterModel (a7, counter.clj:100-127) and LeaderModel
+// (leader.clj:63-75, on the counter's config layout; encode.hpp C_LEADER) as one persistent, cooperative, level-synchronous kernel on gfx950.
 //
 // Layout and algorithm:
 //  * A config (model state, linearized bits of the live pending slots) of history h is a
@@ -262,13 +262,18 @@ __global__ void __launch_bounds__(BLOCK) search_kernel(SearchParams p) {
           const int64_t a = oa[q], d = ob[q];
           const int64_t st = e.st;
           int64_t r;
-          bool ovf = (kind & 4) ? __builtin_sub_overflow(st, d, &r) : __builtin_add_overflow(st, d, &r);
-          if (ovf) {  // Clojure +/- throw -> the checker errors -> :valid? :unknown
-            atomicCAS(&p.status[h], ST_RUNNING, ST_MODEL);
-            continue;
+          if (kind & 8) {  // LeaderModel.step (leader.clj:69-75): a term's other leader -> inconsistent
+            if (st & a) continue;
+            r = st | d;
+          } else {
+            bool ovf = (kind & 4) ? __builtin_sub_overflow(st, d, &r) : __builtin_add_overflow(st, d, &r);
+            if (ovf) {  // Clojure +/- throw -> the checker errors -> :valid? :unknown
+              atomicCAS(&p.status[h], ST_RUNNING, ST_MODEL);
+              continue;
+            }
+            if ((kind & 1) && st != a) continue;
+            if ((kind & 2) && r != a) continue;
           }
-          if ((kind & 1) && st != a) continue;
-          if ((kind & 2) && r != a) continue;
           ne.key = ((key | (1ull << k)) & tag_clear) | tag_now;
           ne.st = r;
         }

@@ -82,7 +82,7 @@ def final_paths(model: Model, configs, pending, fail_inv: int, ops, k: int = 10)
         return []
     order = sorted(pending)
     paths = []
-    queue = [((None if s is None else s) if model.name == "cas-register" else (s or 0),
+    queue = [((None if s is None else s) if model.name in ("cas-register", "leader") else (s or 0),
               frozenset(lin), [{"op": None, "model": {"value": s}}]) for (s, lin) in configs]
     while queue and len(paths) < k:
         nxt = []
@@ -103,6 +103,35 @@ def final_paths(model: Model, configs, pending, fail_inv: int, ops, k: int = 10)
     return paths
 
 
+def _leader_maps(ops, fail_idx: int, cfgs):
+    """LeaderModel configs: the device reports each config's contested pairs only, so its
+    term -> leader map is rebuilt as the search defines it: the (term, leader) pairs of every
+    op that returned :ok before the failing completion, plus the pending ops the config has
+    linearized (leader.clj:69-75: a consistent map has one leader per term)."""
+    folded = _folded_ops(ops)
+    returned, by_proc = [], {}
+    for pos, o in enumerate(ops):
+        idx = int(o.get("index", pos))
+        if idx == fail_idx:
+            break
+        t = str(o.get("type", "")).lstrip(":")
+        if t == "invoke":
+            by_proc[o.get("process")] = idx
+        elif o.get("process") in by_proc:
+            inv = by_proc.pop(o.get("process"))
+            if t == "ok":
+                returned.append(inv)
+    out = []
+    for _s, lin in cfgs:
+        state = None
+        for i in returned + sorted(lin):
+            fo = folded.get(i)
+            if fo is not None:
+                state = step(Model("leader", 3), state, "inspect", fo["value"])
+        out.append((state or {}, lin))
+    return out
+
+
 def _result_map(ops, r, k, model: Model, configs=None) -> Dict[str, Any]:
     v = VALID[int(r["valid"][k])]
     out: Dict[str, Any] = {"valid?": v, "analyzer": "linear",
@@ -121,6 +150,8 @@ def _result_map(ops, r, k, model: Model, configs=None) -> Dict[str, Any]:
         out["last-op"] = out["previous-ok"]
         if configs is not None:
             cfgs, pending, lasts, newest = configs
+            if model.name == "leader":
+                cfgs = _leader_maps(ops, int(r["fail_idx"][k]), cfgs)
             out["last-op"] = _op_at(ops, newest)
             # Knossos :configs [ext]: {:model :last-op :pending}, :pending = the calls this
             # config has not linearized (invocations, :index order)
@@ -178,11 +209,11 @@ class Linearizable(Checker):
 
 
 def fallback_result(model: Model) -> Dict[str, Any]:
-    """The map a model the GPU search does not implement gets: the
-    :election workload's LeaderModel (leader.clj:63-85) keeps an unbounded term -> leader map,
-    so the JVM binding routes it to knossos.linear/analysis unchanged. This
-    host mirror has no Knossos to route to and reports the hand-off as :unknown, the shape
-    jepsen's check-safe gives a checker that cannot decide [ext]."""
+    """The map a model the GPU search does not implement gets (a Model(gpu=False); every model
+    the suite uses, LeaderModel included since r3, is searched on the GPU): the JVM binding
+    routes such a model to knossos.linear/analysis unchanged. This host
+    mirror has no Knossos to route to and reports the hand-off as :unknown, the shape jepsen's
+    check-safe gives a checker that cannot decide [ext]."""
     return {"valid?": "unknown", "analyzer": "linear", "fallback": "knossos",
             "error": f"model {model.name} is not searched on the GPU: route it to "
                      "knossos.linear/analysis (the JVM binding's fallback)"}

@@ -9,8 +9,11 @@ Mirrors the op shapes the reference's clients produce:
   * error classification (client.clj:52-63): timeouts of non-idempotent ops -> :info
 
 Encoding (include/lincheck.h): type 0 invoke / 1 ok / 2 fail / 3 info;
-f 0 read / 1 write / 2 cas / 3 add / 4 decr / 5 add-and-get / 6 decr-and-get;
+f 0 read / 1 write / 2 cas / 3 add / 4 decr / 5 add-and-get / 6 decr-and-get / 7 inspect;
 vflags 0 nil / 1 scalar (v0) / 2 pair (v0, v1).
+  * election (leader.clj:14-17, :38-40): :inspect invokes with [nil 0], completes with
+    [leader term ...]; encoded as the pair (leader id, term), the id interned per process from
+    serialize-leader's name (nil and "null" -> -1, leader.clj:51-54)
 """
 from __future__ import annotations
 
@@ -22,7 +25,7 @@ import numpy as np
 TYPE_CODES = {"invoke": 0, "ok": 1, "fail": 2, "info": 3}
 TYPE_NAMES = {v: k for k, v in TYPE_CODES.items()}
 F_CODES = {"read": 0, "write": 1, "cas": 2, "add": 3, "decr": 4,
-           "add-and-get": 5, "decr-and-get": 6}
+           "add-and-get": 5, "decr-and-get": 6, "inspect": 7}
 F_NAMES = {v: k for k, v in F_CODES.items()}
 V_NIL, V_SCALAR, V_PAIR = 0, 1, 2
 
@@ -40,6 +43,30 @@ def tuple_(k, v) -> KV:
 def _kw(x) -> str:
     s = str(x)
     return s[1:] if s.startswith(":") else s
+
+
+F_INSPECT = F_CODES["inspect"]
+_LEADER_IDS: Dict[str, int] = {"null": -1}
+_LEADER_NAMES: Dict[int, Optional[str]] = {-1: None}
+
+
+def leader_id(addr) -> int:
+    """The id of serialize-leader(addr) (leader.clj:51-54): equal names, equal ids."""
+    name = "null" if addr is None else str(addr)
+    i = _LEADER_IDS.get(name)
+    if i is None:
+        i = _LEADER_IDS[name] = len(_LEADER_IDS) - 1
+        _LEADER_NAMES[i] = name
+    return i
+
+
+def _encode_inspect(v):
+    """[leader term ...] -> (V_PAIR, leader id, term); nil stays nil ((leader nil, term nil))."""
+    if v is None:
+        return V_NIL, 0, 0
+    if not isinstance(v, (list, tuple)) or len(v) < 2 or v[1] is None:
+        raise ValueError(f":inspect value must be [leader term ...], got {v!r}")
+    return V_PAIR, leader_id(v[0]), int(v[1])
 
 
 def _encode_value(v):
@@ -96,6 +123,8 @@ class History:
             vf = int(self.vflags[i])
             v = None if vf == V_NIL else (int(self.v0[i]) if vf == V_SCALAR
                                           else [int(self.v0[i]), int(self.v1[i])])
+            if int(self.f[i]) == F_INSPECT and vf == V_PAIR:
+                v = [_LEADER_NAMES.get(int(self.v0[i])), int(self.v1[i])]
             out.append({"process": int(self.process[i]), "index": int(self.index[i]),
                         "type": TYPE_NAMES[int(self.type[i])], "f": F_NAMES[int(self.f[i])],
                         "value": v})
@@ -132,11 +161,12 @@ def encode(ops: Iterable[Dict[str, Any]], unwrap_key: bool = False) -> History:
         v = op.get("value")
         if unwrap_key and isinstance(v, KV):
             v = v.value
-        vf, x, y = _encode_value(v)
+        f = F_CODES[_kw(op["f"])]
+        vf, x, y = _encode_inspect(v) if f == F_INSPECT else _encode_value(v)
         idx.append(int(op.get("index", pos)))
         proc.append(int(op["process"]))
         typ.append(TYPE_CODES[_kw(op["type"])])
-        fs.append(F_CODES[_kw(op["f"])])
+        fs.append(f)
         a0.append(x)
         a1.append(y)
         vfl.append(vf)

@@ -5,9 +5,9 @@
 * CounterModel(v) -> jepsen.jgroups.workload.counter/CounterModel, counter.clj:100-127
                      (used as (CounterModel. 0), counter.clj:136)
 * LeaderModel()   -> jepsen.jgroups.workload.leader/LeaderModel, leader.clj:63-75 (used as
-                     (LeaderModel. {}), leader.clj:84). Out of the GPU's scope (unbounded
-                     term -> leader map state): linearizable() returns
-                     the fallback map, and the JVM binding hands it to Knossos unchanged.
+                     (LeaderModel. {}), leader.clj:84; the :election workload). The GPU search
+                     keeps its term -> leader map as the set of linearized (term, leader) pairs
+                     of the terms that carry two or more leaders (include/lincheck.h).
 """
 from dataclasses import dataclass
 
@@ -33,7 +33,12 @@ def CounterModel(value: int = 0) -> Model:  # noqa: N802  (mirrors the Clojure r
 def LeaderModel(state=None) -> Model:  # noqa: N802  (mirrors the Clojure record name)
     if state:
         raise ValueError("LeaderModel starts from the empty term map, as (LeaderModel. {}) does")
-    return Model("leader", 0, 0, gpu=False)
+    return Model("leader", 3, 0)
+
+
+def serialize_leader(addr) -> str:
+    """leader.clj:51-54: nil -> "null", else the name."""
+    return "null" if addr is None else str(addr)
 
 
 class Inconsistent(str):
@@ -46,8 +51,9 @@ def step(model: Model, value, f: str, v):
     cas [cur new] -> new iff cur = value; read v -> value iff v is nil or v = value.
     CounterModel (counter.clj:100-127): add d -> value + d; decr d -> value - d; read x ->
     value iff x nil or x = value; add-and-get [d n] -> n iff value + d = n (scalar d, the
-    :info case: value + d); decr-and-get mirrors it with -. Returns the new value or an
-    Inconsistent message."""
+    :info case: value + d); decr-and-get mirrors it with -. LeaderModel (leader.clj:69-75):
+    inspect [l t] -> the map with t -> l, inconsistent when it holds t with another leader.
+    Returns the new value or an Inconsistent message."""
     if model.name == "cas-register":
         if f == "write":
             return v
@@ -68,4 +74,14 @@ def step(model: Model, value, f: str, v):
                 return n if value + sign * d == n else Inconsistent(
                     f"{'adding' if sign > 0 else 'decreasing'} {d} to {value} should result in {n}")
             return value + sign * v
+    elif model.name == "leader":
+        # LeaderModel.step (leader.clj:69-75) on the term -> leader map (None: {})
+        if f == "inspect":
+            state = dict(value or {})
+            inspected, t = (v[0], v[1]) if v is not None else (None, None)
+            l = serialize_leader(inspected)
+            if t in state and state[t] != l:
+                return Inconsistent(f"leader at {t} was {state[t]} but received {l}")
+            state[t] = l
+            return state
     return Inconsistent(f"unknown :f {f} for {model.name}")

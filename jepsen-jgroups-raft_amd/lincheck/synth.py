@@ -20,9 +20,9 @@ from __future__ import annotations
 
 import numpy as np
 
-from .history import History, V_NIL, V_PAIR, V_SCALAR, concat, from_columns
+from .history import History, V_NIL, V_PAIR, V_SCALAR, concat, from_columns, leader_id
 
-F_READ, F_WRITE, F_CAS, F_ADD, F_DECR, F_AAG, F_DAG = range(7)
+F_READ, F_WRITE, F_CAS, F_ADD, F_DECR, F_AAG, F_DAG, F_INSPECT = range(8)
 T_INV, T_OK, T_FAIL, T_INFO = range(4)
 
 
@@ -183,6 +183,44 @@ def gen_counter(n_ops: int, n_clients: int, p_info: float, seed: int,
     c_b = np.where(get, res, zeros)
     return _emit(n_clients, client, inv, cmp_, typ, fs, (inv_vf, inv_a, zeros),
                  (c_vf, c_a, c_b), crashed)
+
+
+def gen_leader(n_ops: int, n_clients: int, p_info: float, seed: int, invalid: bool = False,
+               n_terms: int = 6, n_nodes: int = 5, p_crash: float = 0.0) -> History:
+    """The :election workload (leader.clj:14-17, :38-40, :79-85): every op is :inspect, invoked
+    with [nil 0] and completed with the [leader term] the cluster reports at its linearization
+    point. Ground truth: term 0 without a leader ("null"), then terms 1..n_terms, each with one
+    leader among n_nodes nodes ("n0".., interned ids), elections spread over the run. An
+    inspect that times out is :fail (idempotent, client.clj:52-63), with probability p_info;
+    p_crash > 0 also leaves ops :info (pending forever with their [nil 0] invoke value), to
+    exercise the search's pending-op paths. invalid=True gives one :ok op of a term another
+    :ok op also reports a different leader (a second leader in one term)."""
+    rng = np.random.default_rng(seed)
+    fs = np.full(n_ops, F_INSPECT, np.int8)
+    client, inv, cmp_, lin, crashed, read_fail, _ = _schedule(rng, n_ops, n_clients, 0.0, fs)
+    horizon = float(cmp_.max()) if n_ops else 1.0
+    t_elect = np.sort(rng.uniform(0.0, horizon, n_terms))
+    leaders = [leader_id(f"n{int(k)}") for k in rng.integers(0, n_nodes, n_terms)]
+    term = np.searchsorted(t_elect, lin, side="right")  # 0 before the first election
+    lead = np.array([leader_id(None)] + leaders, np.int64)[term]
+    typ = np.full(n_ops, T_OK, np.int8)
+    u = rng.uniform(size=n_ops)
+    typ[u < p_info] = T_FAIL
+    crashed = (u >= p_info) & (u < p_info + p_crash)
+    typ[crashed] = T_INFO
+    if invalid:
+        ok = np.nonzero(typ == T_OK)[0]
+        terms_ok = term[ok]
+        multi = [i for i in ok if np.count_nonzero(terms_ok == term[i]) >= 2]
+        if multi:
+            j = multi[rng.integers(0, len(multi))]
+            others = [leader_id(f"n{k}") for k in range(n_nodes) if leader_id(f"n{k}") != lead[j]]
+            lead[j] = others[rng.integers(0, len(others))]
+    zeros = np.zeros(n_ops, np.int64)
+    pair = np.full(n_ops, V_PAIR, np.int8)
+    inv_v = (pair, np.full(n_ops, leader_id(None), np.int64), zeros)  # [nil 0]
+    cmp_v = (pair, lead.astype(np.int64), term.astype(np.int64))
+    return _emit(n_clients, client, inv, cmp_, typ, fs, inv_v, cmp_v, crashed)
 
 
 def gen_register_keys(n_keys: int, ops_per_key: int, n_clients: int, p_info: float,

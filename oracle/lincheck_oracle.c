@@ -6,7 +6,7 @@
  *   -> knossos.history preprocessing  [ext, knossos via jepsen 0.3.5, project.clj:11]
  *   -> knossos.linear/analysis        [ext] just-in-time linearization search (Lowe 2017)
  *   -> model step: knossos.model/CASRegister [ext] (register.clj:110), CounterModel
- *      (counter.clj:100-127)
+ *      (counter.clj:100-127), LeaderModel (leader.clj:63-75, the :election workload)
  * Knossos is a third-party JVM dependency that is absent from /root/reference and from
  * this image (no JVM, no jar); its published algorithm is restated here. Counter parity is
  * pinned by the reference's KATs (test/jepsen/jgroups/raft_test.clj:6-65); cas-register
@@ -42,7 +42,15 @@ typedef struct {
   int8_t status; /* 0 none (pending forever), 1 ok, 2 fail, 3 info */
   int8_t f, vflags;
   int64_t v0, v1;
+  int32_t pair; /* LeaderModel: the op's (term, leader) pair in the history's ltab */
 } oop;
+
+/* LeaderModel: the history's distinct (term, leader) pairs, first appearance first. */
+typedef struct {
+  int64_t term[64], leader[64];
+  int8_t tnil[64];
+  int n;
+} ltab;
 
 enum { ST_INCONSISTENT = 0, ST_OK = 1, ST_ERROR = -1 };
 
@@ -113,6 +121,24 @@ static int step_counter(mstate s, const oop* o, mstate* out, const char** why) {
       *why = "unknown :f for CounterModel"; /* condp throws, counter.clj:102 */
       return ST_ERROR;
   }
+}
+
+/* LeaderModel.step, leader.clj:69-75, for (:inspect [leader term]): a map without the term
+ * gains (term -> leader); a map holding the term keeps itself when the leaders are equal and is
+ * inconsistent otherwise ((empty? state) gives the same map as assoc). The map is kept as the
+ * set of its (term, leader) pairs: a bitmask over the history's ltab. Leaders arrive as the
+ * caller's ids of serialize-leader's names (nil = "null" = -1, leader.clj:51-54); a nil value
+ * destructures to (leader nil, term nil). */
+static int step_leader(mstate s, const oop* o, const ltab* L, mstate* out) {
+  const int k = o->pair;
+  for (uint64_t m = (uint64_t)s.value; m; m &= m - 1) {
+    const int q = __builtin_ctzll(m);
+    if (L->tnil[q] == L->tnil[k] && L->term[q] == L->term[k] && L->leader[q] != L->leader[k])
+      return ST_INCONSISTENT;
+  }
+  out->nil = 0;
+  out->value = (int64_t)((uint64_t)s.value | (1ULL << k));
+  return ST_OK;
 }
 
 /* ------------------------------------------------------------------ config hash set */
@@ -254,7 +280,7 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
   memset(out, 0, sizeof(*out));
   out->valid = 1;
   out->fail_idx = out->fail_inv_idx = out->prev_ok_idx = -1;
-  if (model_kind != OR_MODEL_CAS_REGISTER && model_kind != OR_MODEL_COUNTER) {
+  if (model_kind != OR_MODEL_CAS_REGISTER && model_kind != OR_MODEL_COUNTER && model_kind != OR_MODEL_LEADER) {
     set_err(out, -2, "unknown model kind");
     return -2;
   }
@@ -280,7 +306,7 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
       if (*pend >= 0) { set_err(out, -4, "process invoked while an op was outstanding"); rc = -4; break; }
       oop* o = &ops[n_ops];
       o->inv_pos = i; o->cmp_pos = -1; o->status = 0;
-      o->f = f[i]; o->vflags = vflags[i]; o->v0 = v0[i]; o->v1 = v1[i];
+      o->f = f[i]; o->vflags = vflags[i]; o->v0 = v0[i]; o->v1 = v1[i]; o->pair = 0;
       *pend = n_ops; op_of_entry[i] = n_ops; n_ops++;
     } else if (type[i] == OR_OK || type[i] == OR_FAIL || type[i] == OR_INFO) {
       if (*pend < 0) { set_err(out, -4, "completion without an outstanding invocation"); rc = -4; break; }
@@ -307,6 +333,9 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
       else if (o->f == OR_F_CAS && o->vflags != OR_V_PAIR) why = "cas without [cur new]";
       else if (o->f == OR_F_READ && o->vflags == OR_V_PAIR) why = "read with a pair value";
       else if (o->f != OR_F_WRITE && o->f != OR_F_CAS && o->f != OR_F_READ) why = "unknown :f for cas-register";
+    } else if (model_kind == OR_MODEL_LEADER) {
+      if (o->f != OR_F_INSPECT) why = "unknown :f for LeaderModel";
+      else if (o->vflags == OR_V_SCALAR) why = ":inspect value is not [leader term]";
     } else {
       if ((o->f == OR_F_ADD || o->f == OR_F_DECR) && o->vflags != OR_V_SCALAR) why = ":add/:decr need a scalar delta";
       else if (o->f == OR_F_READ && o->vflags == OR_V_PAIR) why = ":read with a pair value";
@@ -314,6 +343,21 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
       else if (o->f < OR_F_READ || o->f > OR_F_DECR_AND_GET || o->f == OR_F_WRITE || o->f == OR_F_CAS) why = "unknown :f for CounterModel";
     }
     if (why) { set_err(out, -6, why); rc = -6; }
+  }
+  ltab LT;
+  LT.n = 0;
+  for (int64_t k = 0; k < n_ops && rc == 0 && model_kind == OR_MODEL_LEADER; ++k) {
+    oop* o = &ops[k];
+    if (o->status == OR_FAIL) continue;
+    const int8_t tn = o->vflags == OR_V_NIL;
+    const int64_t t = tn ? 0 : o->v1, l = tn ? -1 : o->v0;
+    int q = 0;
+    while (q < LT.n && !(LT.tnil[q] == tn && LT.term[q] == t && LT.leader[q] == l)) ++q;
+    if (q == LT.n) {
+      if (LT.n == 64) { set_err(out, -7, "more than 64 distinct (term, leader) pairs (oracle limit)"); rc = -7; break; }
+      LT.tnil[q] = tn; LT.term[q] = t; LT.leader[q] = l; LT.n++;
+    }
+    o->pair = q;
   }
   if (rc) { free(ops); free(op_of_entry); return rc; }
 
@@ -328,7 +372,7 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
    * earlier) keeps its own. Two routes to one config keep the most recent (the closure's). */
   const int track = cfg_cap > 0;
   if (!cset_init(&S, 1024) || !cset_init2(&O, 1024, track)) { set_err(out, -3, "out of memory"); rc = -3; }
-  cfg c0 = {0, init_value, model_kind == OR_MODEL_CAS_REGISTER ? 1 : 0, -1};
+  cfg c0 = {0, model_kind == OR_MODEL_LEADER ? 0 : init_value, model_kind == OR_MODEL_CAS_REGISTER ? 1 : 0, -1};
   if (model_kind == OR_MODEL_CAS_REGISTER) c0.value = 0; /* (cas-register) starts at nil */
   if (!rc) cvec_push(&F, &c0);
   out->max_frontier = 1;
@@ -375,8 +419,9 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
           if (c->mask >> k & 1) continue;
           mstate s = {c->value, c->nil}, s2;
           const char* why = 0;
-          int st = (model_kind == OR_MODEL_CAS_REGISTER) ? step_register(s, &ops[pend_list[k]], &s2, &why)
-                                                         : step_counter(s, &ops[pend_list[k]], &s2, &why);
+          int st = model_kind == OR_MODEL_CAS_REGISTER ? step_register(s, &ops[pend_list[k]], &s2, &why)
+                   : model_kind == OR_MODEL_LEADER     ? step_leader(s, &ops[pend_list[k]], &LT, &s2)
+                                                       : step_counter(s, &ops[pend_list[k]], &s2, &why);
           if (st == ST_ERROR) { set_err(out, -6, why); rc = -6; break; }
           if (st == ST_INCONSISTENT) continue;
           cfg c2 = {c->mask | (1ULL << k), s2.value, s2.nil, (int32_t)pend_list[k]};

@@ -23,10 +23,10 @@ extern "C" {
 #endif
 
 /* Shared encoding (same constants as include/lincheck.h; data, not code). */
-enum { OR_MODEL_CAS_REGISTER = 1, OR_MODEL_COUNTER = 2 };
+enum { OR_MODEL_CAS_REGISTER = 1, OR_MODEL_COUNTER = 2, OR_MODEL_LEADER = 3 };
 enum { OR_INVOKE = 0, OR_OK = 1, OR_FAIL = 2, OR_INFO = 3 };
 enum { OR_F_READ = 0, OR_F_WRITE = 1, OR_F_CAS = 2, OR_F_ADD = 3, OR_F_DECR = 4,
-       OR_F_ADD_AND_GET = 5, OR_F_DECR_AND_GET = 6 };
+       OR_F_ADD_AND_GET = 5, OR_F_DECR_AND_GET = 6, OR_F_INSPECT = 7 };
 enum { OR_V_NIL = 0, OR_V_SCALAR = 1, OR_V_PAIR = 2 };
 
 typedef struct {

@@ -66,7 +66,7 @@ def _p(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-MODEL = {"cas-register": 1, "register": 1, "counter": 2}
+MODEL = {"cas-register": 1, "register": 1, "counter": 2, "leader": 3}
 
 
 def check_one(model: str, h, init_value: int = 0, max_configs: int = 0, with_configs=False):

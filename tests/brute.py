@@ -6,8 +6,8 @@
   linearizable; the JIT search (knossos.linear [ext]) fails exactly there.
 * `literal_search`: a literal restatement of the §8(a) contract with configs as
   (model value, frozenset of linearized op ids) — cross-checks explored/max_frontier.
-Models follow knossos.model/CASRegister [ext] (register.clj:110) and CounterModel
-(counter.clj:100-127).
+Models follow knossos.model/CASRegister [ext] (register.clj:110), CounterModel
+(counter.clj:100-127) and LeaderModel (leader.clj:63-75; state = frozenset of (term, leader)).
 """
 from __future__ import annotations
 
@@ -22,6 +22,15 @@ def _val(op):
 
 def step(model, state, f, v):
     """Returns the next state or None if inconsistent."""
+    if model == "leader":  # leader.clj:69-75 over a frozenset of (term, leader) pairs
+        if f != "inspect":
+            raise ValueError(f)
+        leader, term = (v[0], v[1]) if v is not None else (None, None)
+        name = "null" if leader is None else str(leader)
+        for (t, l) in state:
+            if t == term:
+                return state if l == name else None
+        return state | {(term, name)}
     if model == "cas-register":
         if f == "write":
             return NIL if v is None else v
@@ -68,7 +77,7 @@ def preprocess(history):
 
 
 def _init(model, init_value):
-    return NIL if model == "cas-register" else init_value
+    return NIL if model == "cas-register" else frozenset() if model == "leader" else init_value
 
 
 def brute_valid(model, history, init_value=0, upto=None):

@@ -14,7 +14,7 @@ from lincheck import _lib, checker, history as H, model, synth
 
 pytestmark = pytest.mark.gpu
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kats.json")))
-KIND = {"cas-register": 1, "counter": 2}
+KIND = {"cas-register": 1, "counter": 2, "leader": 3}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -238,6 +238,68 @@ def test_gpu_failure_configs_match_oracle(m):
         carried += sum(1 for x in lasts if x != e["prev_ok_idx"])
         found += 1
     assert found > 5 and carried > 0  # some configs were carried through the last RETURN
+
+
+def _leader_hists(n, seed0, n_ops=200, p_crash=0.03):
+    return [synth.gen_leader(n_ops, 5, 0.05, seed0 + t, invalid=(t % 3 == 1), n_terms=4 + t % 5,
+                             p_crash=p_crash if t % 2 else 0.0) for t in range(n)]
+
+
+@pytest.mark.parametrize("path", [None, "keys", "grid"])
+def test_gpu_leader_vs_oracle(path, monkeypatch):
+    """The :election workload's LeaderModel (leader.clj:63-85) on the GPU search: verdicts,
+    failing ops and explored counts bit-exact with the oracle, invalid histories (a second
+    leader in one term) and crashed ops (pending forever with [nil 0]) included, through the
+    per-key kernel and the grid kernel."""
+    if path:
+        monkeypatch.setenv("LC_PATH", path)
+    h = H.concat(_leader_hists(30, 62000))
+    g = _lib.check(3, 0, h)
+    exp = oracle.check_many("leader", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"leader path={path}")
+    assert any(e["valid"] == 0 for e in exp) and any(e["valid"] == 1 for e in exp)
+
+
+def test_gpu_leader_contested_pair_limit():
+    """More than 64 contested (term, leader) pairs: :unknown with the capacity code (the
+    oracle, whose limit counts every distinct pair, cannot check such a history either)."""
+    ops = []
+    for t in range(33):  # 33 terms, two leaders each: 66 contested pairs
+        for p, name in ((0, "a"), (1, "b")):
+            ops += [{"process": p, "type": "invoke", "f": "inspect", "value": [None, 0]},
+                    {"process": p, "type": "ok", "f": "inspect", "value": [name, t + 1]}]
+    g = _lib.check(3, 0, H.encode(ops))
+    assert int(g["valid"][0]) == 2 and int(g["err"][0]) == -7
+
+
+def test_gpu_leader_failure_report():
+    """Failure report for LeaderModel: the pre-failure configs (as linearized sets: the
+    device holds contested pairs, the oracle every pair) and per-config :last-op match the
+    oracle; the checker's map carries term -> leader maps and final paths ending in the
+    reference's inconsistency message."""
+    from lincheck import checker, model
+    found = 0
+    for t in range(30):
+        h = synth.gen_leader(60, 4, 0.1, 63000 + t, invalid=True, n_terms=3, p_crash=0.1)
+        e = oracle.check_one("leader", h, with_configs=True)
+        g = _lib.check(3, 0, h)
+        assert int(g["valid"][0]) == e["valid"]
+        if e["valid"] != 0:
+            continue
+        cfgs, pending, lasts, newest = _lib.failure_configs(0, 1 << 12, with_last=True)
+        assert sorted(pending) == sorted(e["pending_inv_idx"])
+        got = {lin: last for (_s, lin), last in zip(cfgs, lasts)}
+        want = {lin: e["fail_last_op"][(s, lin)] for (s, lin) in e["fail_configs"]}
+        assert got == want and len(cfgs) == len(e["fail_configs"])
+        res = checker.linearizable({"model": model.LeaderModel()}).check({}, h.to_ops(), {})
+        assert res["valid?"] is False and res["op"]["index"] == e["fail_idx"]
+        for c in res["configs"]:
+            assert isinstance(c["model"]["value"], dict)
+        assert res["final-paths"] and all("but received" in p[-1]["model"]["inconsistent"]
+                                          for p in res["final-paths"])
+        found += 1
+    assert found > 5
 
 
 def test_gpu_counter_bounds_vs_oracle():

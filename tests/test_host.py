@@ -26,7 +26,7 @@ def test_library_exports_every_symbol():
     L = _lib.load()
     for s in _declared():
         assert hasattr(L, s), s
-    assert L.lc_abi_version() == _lib.ABI_VERSION == 2
+    assert L.lc_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_no_device_fails_loudly():
@@ -295,14 +295,49 @@ def test_shard_histories_rejects_bad_args():
     assert L.lc_shard_histories(2, _lib._p(np.array([0, 1, 2], np.int64)), 0, _lib._p(out)) == -1
 
 
-def test_leader_model_routes_to_fallback():
-    """the :election workload's LeaderModel (leader.clj:63-85) is not
-    searched on the GPU; linearizable() hands back the documented fallback map."""
-    c = checker.linearizable({"model": model.LeaderModel(), "algorithm": "linear"})
-    r = c.check({}, [{"process": 0, "type": "invoke", "f": "inspect", "value": None, "index": 0}])
-    assert r["valid?"] == "unknown" and r["fallback"] == "knossos" and "error" in r
+def test_leader_model_is_searched_natively():
+    """SURVEY §8(f) row 3, done natively since r3: LeaderModel (leader.clj:63-85) is model kind
+    3 of the C ABI; only a Model(gpu=False) still gets the fallback map."""
+    m = model.LeaderModel()
+    assert m.gpu and m.kind == 3 and m.name == "leader"
     with pytest.raises(ValueError):
         model.LeaderModel({1: "n1"})
+    r = checker.fallback_result(model.Model("other", 0, gpu=False))
+    assert r["valid?"] == "unknown" and r["fallback"] == "knossos" and "error" in r
+
+
+def test_leader_failure_report_shape_from_oracle_configs():
+    """The checker's LeaderModel failure report, fed the oracle's pre-failure configs (the GPU
+    test feeds the device's): configs carry term -> leader maps rebuilt from the returned and
+    linearized ops, final paths end in the reference's message (leader.clj:73)."""
+    import oracle
+    from lincheck import synth
+    done = 0
+    for t in range(40):
+        h = synth.gen_leader(60, 4, 0.1, 63000 + t, invalid=True, n_terms=3, p_crash=0.1)
+        e = oracle.check_one("leader", h, with_configs=True)
+        if e["valid"] != 0:
+            continue
+        r = {"valid": np.array([0]), "explored": np.array([e["explored"]]), "err": np.array([0]),
+             "fail_idx": np.array([e["fail_idx"]]), "prev_ok": np.array([e["prev_ok_idx"]]),
+             "fail_inv": np.array([e["fail_inv_idx"]])}
+        cfgs = sorted(e["fail_configs"])
+        lasts = [e["fail_last_op"][c] for c in cfgs]
+        res = checker._result_map(h.to_ops(), r, 0, model.LeaderModel(),
+                                  (cfgs, e["pending_inv_idx"], lasts, max(lasts)))
+        op = res["op"]
+        assert op["index"] == e["fail_idx"] and op["f"] == "inspect"
+        for c in res["configs"]:
+            m = c["model"]["value"]
+            assert isinstance(m, dict) and all(isinstance(v, str) for v in m.values())
+            # the failing op's term already has another leader in every config
+            assert m.get(op["value"][1]) not in (None, op["value"][0])
+        assert res["final-paths"]
+        for p in res["final-paths"]:
+            assert p[-1]["op"]["index"] == e["fail_inv_idx"]
+            assert "but received" in p[-1]["model"]["inconsistent"]
+        done += 1
+    assert done > 5
 
 
 def test_independent_failures_exclude_unknown():

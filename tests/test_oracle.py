@@ -38,11 +38,14 @@ def test_brute_agrees_with_kats(kat):
 
 
 def _small_random(model, seed, n_ops, clients, p_info, invalid):
+    if model == "leader":
+        return synth.gen_leader(n_ops, clients, p_info, seed, invalid=invalid, n_terms=2,
+                                n_nodes=3, p_crash=0.25)
     g = synth.gen_register if model == "cas-register" else synth.gen_counter
     return g(n_ops, clients, p_info, seed, invalid=invalid)
 
 
-@pytest.mark.parametrize("model", ["cas-register", "counter"])
+@pytest.mark.parametrize("model", ["cas-register", "counter", "leader"])
 def test_oracle_vs_brute_random(model):
     rng = random.Random(7)
     checked = 0
@@ -62,13 +65,16 @@ def test_oracle_vs_brute_random(model):
     assert checked == 120
 
 
-@pytest.mark.parametrize("model", ["cas-register", "counter"])
+@pytest.mark.parametrize("model", ["cas-register", "counter", "leader"])
 def test_oracle_vs_literal_medium(model):
     """Larger random histories (no brute force): the literal restatement must agree on
     verdict, failing index, explored count and max frontier."""
     for t in range(12):
-        g = synth.gen_register if model == "cas-register" else synth.gen_counter
-        h = g(60, 4, 0.05, 5000 + t, invalid=(t % 3 == 2))
+        if model == "leader":
+            h = synth.gen_leader(60, 4, 0.05, 5000 + t, invalid=(t % 3 == 2), p_crash=0.05)
+        else:
+            g = synth.gen_register if model == "cas-register" else synth.gen_counter
+            h = g(60, 4, 0.05, 5000 + t, invalid=(t % 3 == 2))
         ops = h.to_ops()
         r = oracle.check_one(model, h)
         lit = literal_search(model, ops)
@@ -158,3 +164,53 @@ def test_oracle_failure_last_ops_vs_literal(model):
             n_cfg += 1
             n_multi += len(lasts) > 1
     assert n_cfg > 50 and n_multi > 0, (n_cfg, n_multi)
+
+
+def test_leader_model_step_literal():
+    """LeaderModel.step (leader.clj:69-75) on literal maps: the empty map takes any term; a held
+    term keeps the map for its own leader and is inconsistent for another; nil leaders
+    serialize to "null" (leader.clj:51-54), so [nil t] and ["null" t] agree."""
+    from lincheck import model as M
+    L = M.LeaderModel()
+    s = M.step(L, None, "inspect", ["n1", 3])
+    assert s == {3: "n1"}
+    assert M.step(L, s, "inspect", ["n1", 3]) == {3: "n1"}
+    assert isinstance(M.step(L, s, "inspect", ["n2", 3]), M.Inconsistent)
+    assert "leader at 3 was n1 but received n2" == str(M.step(L, s, "inspect", ["n2", 3]))
+    assert M.step(L, s, "inspect", [None, 4]) == {3: "n1", 4: "null"}
+    assert M.step(L, {4: "null"}, "inspect", ["null", 4]) == {4: "null"}
+    assert M.step(L, {}, "inspect", None) == {None: "null"}
+
+
+def test_leader_encoding_round_trip():
+    """:inspect values encode as (leader id, term) pairs, nil and "null" to one id, and decode
+    back to names."""
+    ops = [{"process": 0, "type": "invoke", "f": "inspect", "value": [None, 0]},
+           {"process": 0, "type": "ok", "f": "inspect", "value": ["n1", 2, "extra"]},
+           {"process": 1, "type": "invoke", "f": "inspect", "value": [None, 0]},
+           {"process": 1, "type": "ok", "f": "inspect", "value": ["null", 2]}]
+    h = H.encode(ops)
+    assert list(h.f) == [7] * 4 and list(h.vflags) == [2] * 4
+    assert h.v0[0] == h.v0[2] == h.v0[3] == -1 and h.v0[1] >= 0 and list(h.v1) == [0, 2, 0, 2]
+    back = h.to_ops()
+    assert back[1]["value"] == ["n1", 2] and back[3]["value"] == [None, 2]
+    r = oracle.check_one("leader", h)  # (2, n1) and (2, null): a second leader for term 2
+    assert r["valid"] == 0 and r["fail_idx"] == 3 and brute_valid("leader", ops) is False
+
+
+def test_leader_oracle_failure_configs_vs_literal():
+    """Failure report configs and per-config :last-op for LeaderModel histories, against the
+    literal search (its states are term maps, the oracle's pair bitmasks; a config's state is a
+    function of its linearized set, so configs compare by that set)."""
+    n = 0
+    for t in range(120):
+        h = synth.gen_leader(30, 4, 0.1, 8800 + t, invalid=True, n_terms=3, p_crash=0.15)
+        r = oracle.check_one("leader", h, with_configs=True)
+        if r["valid"] != 0:
+            continue
+        lit = literal_last_ops("leader", h.to_ops())
+        got = {lin: r["fail_last_op"][(s, lin)] for (s, lin) in r["fail_configs"]}
+        want = {lin: max(-1 if x is None else x for x in lasts) for (_s, lin), lasts in lit.items()}
+        assert got == want, t
+        n += 1
+    assert n > 40
