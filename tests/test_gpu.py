@@ -103,11 +103,12 @@ def test_gpu_c2_full_size_vs_oracle():
     _cmp(g, oracle.check_one("cas-register", h), 0, "c2-full")
 
 
-# C4 (BASELINE configs[3]): one 100k-op history with crashed :info ops, width 23 (beyond the
-# dense tables: the grid kernel). Its explored count, found identical by the grid kernel and
-# by the partitioned search (csrc/part.hip) in round 1, is pinned here; the oracle covers the
-# longest prefix it finishes in ~20 s.
-C4_EXPLORED = 10_994_841_001
+# C4 (BASELINE configs[3]): one 100k-op history with crashed :info ops. Its full-size oracle
+# verdict and explored count (tests/golden/c4_oracle.json: the C oracle on one thread, 3.0 h,
+# made by tests/golden/pin_c4.py) are the fixture every GPU path must reproduce.
+C4_GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c4_oracle.json")))
+C4_EXPLORED = C4_GOLD["explored"]
+assert C4_GOLD["valid"] == 1 and C4_GOLD["err_code"] == 0 and C4_GOLD["n_ops"] == 100_000
 
 
 def test_gpu_c4_full_size_grid(monkeypatch):

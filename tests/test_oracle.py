@@ -214,3 +214,15 @@ def test_leader_oracle_failure_configs_vs_literal():
         assert got == want, t
         n += 1
     assert n > 40
+
+
+def test_c4_fixture_matches_generator():
+    """tests/golden/c4_oracle.json (the full-size C4 oracle run, tests/golden/pin_c4.py) was
+    made from this generator's C4 history: same entry and op counts, and its first 4k entries
+    check the same way here (the GPU suite compares every path's explored count with it)."""
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c4_oracle.json")))
+    h = synth.gen_config("c4")
+    assert (h.n, h.n_ops()) == (gold["n_entries"], gold["n_ops"])
+    assert gold["valid"] == 1 and gold["explored"] == 10_994_841_001
+    r = oracle.check_one("cas-register", synth.truncate(h, 4000))
+    assert r["valid"] == 1 and r["explored"] > 0
