@@ -350,6 +350,7 @@ struct lc_plan {
     if ((e = getenv("LC_PLAN_X")) && atof(e) > 0) plan_x = atof(e);
     if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
     if ((e = getenv("LC_TEAM_ROT_LB"))) rot_min_lb = atoi(e);
+    if ((e = getenv("LC_TEAM_ROT_CHAIN"))) rot_chain_lb = atoi(e);
     if ((e = getenv("LC_BATCH_HIST"))) batch_hist = atoi(e);
     if ((e = getenv("LC_MID_MAXW")) && atoi(e) > DENSE_WAVE_LMAX && atoi(e) <= DENSE_MID_LMAX) mid_maxw = atoi(e);
     if ((e = getenv("LC_TILE_WIDE")) && strchr(e, ':')) {
@@ -374,7 +375,7 @@ struct lc_plan {
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 4047, pipe_env = false, plan_off = false;
-    plan_k16 = -1, plan_x = 1.57, team_rot = -1, rot_min_lb = 16, batch_hist = 600, mid_maxw = 0;
+    plan_k16 = -1, plan_x = 1.57, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
     rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
     kfcap = klcap = 1 << 18;
     cell_cap = 256;
@@ -620,7 +621,12 @@ struct lc_plan {
           int wide = 0;
           for (int L = lb + 1; L <= 32; ++L) wide += (int)widths[h].c[L];
           const bool mostly_wide = 10 * wide >= 4 * (int)widths[h].steps();
-          if (lb < rot_min_lb || !(batch_plan() || mostly_wide)) continue;
+          // a chain plan's widest teams (14-slot tiles, >= 4 team bits: 16+ tiles) gain from it
+          // too (r3i, every 8-way C3 share rotated and not: w21/lb14 8.46 -> 7.37 ms and 6.64 ->
+          // 6.22, w18/lb14 6.24 -> 5.91; w17/lb14 (3 team bits) 6.62 -> 6.86, and 13-slot tiles
+          // lose at every width: w19/lb13 6.39 -> 7.08, w20/lb13 6.34 -> 7.05)
+          const bool chain_widest = !batch_plan() && lb == rot_chain_lb && lw - lb >= 4;
+          if (!chain_widest && (lb < rot_min_lb || !(batch_plan() || mostly_wide))) continue;
         }
         const int r = team_rot < 0 ? lw - lb : std::min(team_rot, lw - lb);
         if (r <= 0) continue;
@@ -714,6 +720,7 @@ struct lc_plan {
   uint32_t mirror_seq = 0;  // tagged mirrors: launches since the buffer was last zeroed
   int team_rot = -1;       // LC_TEAM_ROT: tile-team slot rotation (build_dense; -1 auto)
   int rot_min_lb = 16;     // LC_TEAM_ROT_LB: auto rotation from this tile size
+  int rot_chain_lb = 14;   // LC_TEAM_ROT_CHAIN: a chain plan's teams of this tile size (>= 4 team bits)
   // rotation keeps slots 0..2 in the word (the encoder's slot policy; LC_SLOTS=lff: rotate them too)
   bool rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
   // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7); by default 14 for
