@@ -30,7 +30,7 @@ def seed_for(config_id: int, key: int) -> int:
     return 0x5EED0000 + config_id * 1000 + key
 
 
-def _schedule(rng, n_ops, n_clients, p_info, fs):
+def _schedule(rng, n_ops, n_clients, p_info, fs, crash_idx=None):
     """Per-op timing for n_ops ops spread over n_clients back-to-back clients."""
     per = np.full(n_clients, n_ops // n_clients)
     per[: n_ops % n_clients] += 1
@@ -50,6 +50,9 @@ def _schedule(rng, n_ops, n_clients, p_info, fs):
     cmp_ = inv + lat
     lin = inv + rng.uniform(0.0, 1.0, n_ops) * lat
     crashed = (fs != F_READ) & (rng.uniform(size=n_ops) < p_info)
+    if crash_idx is not None:  # exactly these (non-read) ops crash (the crash ramp)
+        crashed = np.zeros(n_ops, bool)
+        crashed[np.asarray(crash_idx, np.int64)] = True
     read_fail = (fs == F_READ) & (rng.uniform(size=n_ops) < p_info)
     applied_if_crashed = rng.uniform(size=n_ops) < 0.5
     # a crashed op may take effect late (after its completion time)
@@ -94,12 +97,21 @@ def _emit(n_clients, client, inv, cmp_, typ, fs, inv_v, cmp_v, crashed):
 
 
 def gen_register(n_ops: int, n_clients: int, p_info: float, seed: int,
-                 invalid: bool = False) -> History:
+                 invalid: bool = False, n_crashed: int | None = None,
+                 crash_span: float = 0.2) -> History:
+    """n_crashed: exactly that many write/cas ops time out (:info), drawn uniformly from the
+    first `crash_span` of the ops (the crash ramp); p_info then only makes reads
+    :fail. Default (None): every non-read op crashes with probability p_info."""
     rng = np.random.default_rng(seed)
     fs = rng.integers(0, 3, n_ops).astype(np.int8)  # read / write / cas
     val = rng.integers(0, 5, n_ops)
     old = rng.integers(0, 5, n_ops)
-    client, inv, cmp_, lin, crashed, read_fail, app_c = _schedule(rng, n_ops, n_clients, p_info, fs)
+    crash_idx = None
+    if n_crashed is not None:
+        span = np.nonzero(fs[:max(1, int(n_ops * crash_span))] != F_READ)[0]
+        crash_idx = np.random.default_rng(seed ^ 0xC4A5).choice(span, min(n_crashed, len(span)), replace=False)
+    client, inv, cmp_, lin, crashed, read_fail, app_c = _schedule(rng, n_ops, n_clients, p_info, fs,
+                                                                  crash_idx)
     typ = np.full(n_ops, T_OK, np.int8)
     res = np.zeros(n_ops, np.int64)
     res_nil = np.zeros(n_ops, bool)
