@@ -124,6 +124,21 @@ def test_synth_shapes_follow_reference_domains():
             pend[p] = False
 
 
+def test_synth_exact_crash_count():
+    """The crash ramp's generator (tools/crash_ramp.py): exactly K write/cas ops crash, all in
+    the first crash_span of the ops, the history stays linearizable, and n_crashed=None leaves
+    the p_info draw (every BASELINE config's history) untouched."""
+    for k in (0, 3, 9):
+        h = synth.gen_register(400, 8, 0.01, 40 + k, n_crashed=k)
+        info = np.nonzero(h.type == 3)[0]
+        assert len(info) == k
+        assert np.all(h.f[info] != 0)
+        assert oracle.check_one("cas-register", h)["valid"] == 1
+    a, b = synth.gen_register(300, 5, 0.05, 9), synth.gen_register(300, 5, 0.05, 9, n_crashed=None)
+    for x, y in zip(a.arrays(), b.arrays()):
+        assert np.array_equal(x, y)
+
+
 def test_seeds_follow_survey():
     assert synth.seed_for(3, 7) == 0x5EED0000 + 3007
 
