@@ -206,8 +206,11 @@ struct lc_plan {
   // in-word return starts one super-layer after its predecessor, not two); bit 10 = WAVE
   // histories of at most 9 slots in one wave's registers; bit 11 = their closure as a whole-table
   // fixpoint for steps of at most 7 slots (r3d A/B, 3 runs each: C1 0.523 -> 0.428 ms, C3 11.57
-  // -> 11.59 ms). Default 4047 = 1|2|4|8|64|128|256|512|1024|2048, with the planner.
-  int dense_pipe = 4047;
+  // -> 11.59 ms); bit 12 = X of a step after a hi return from its inputs (off); bit 13 = tile
+  // teams on global popcount layers (off); bit 14 = XCD-compact workgroup roles in the big
+  // kernel (r3l A/B, 2 runs each: C3 11.64 -> 11.55 ms, C2 and 8-way shares unchanged).
+  // Default 20431 = 1|2|4|8|64|128|256|512|1024|2048|16384, with the planner.
+  int dense_pipe = 20431;
   bool pipe_env = false;  // LC_PIPE given: its bits as they are
   std::vector<int> plan_lb;  // team planner: local slots per tile (0: not a team)
   bool plan_off = false;     // LC_TEAM_PLAN=0: every wide history keeps 17-bit tiles
@@ -374,7 +377,7 @@ struct lc_plan {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_from = 99, wide_lbits = DENSE_LMAX;
-    dense_pipe = 4047, pipe_env = false, plan_off = false;
+    dense_pipe = 20431, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.57, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
     rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
     kfcap = klcap = 1 << 18;

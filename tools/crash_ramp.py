@@ -41,19 +41,29 @@ def make(ops: int, clients: int, k: int):
 
 
 def width_of(h) -> int:
-    """Most ops pending at once (crashed ones never complete), as knossos.history sees them."""
+    """Most ops pending at once as the search sees them: an op that completes :fail never enters
+    it, a crashed (:info) one stays pending for ever (the encoder's live width, `encode.cpp`)."""
     import numpy as np
     t = np.asarray(h.type)
     p = np.asarray(h.process)
-    live, best, open_ = 0, 0, {}
+    fails, open_ = set(), {}
+    for i in range(len(t)):  # which invocations end :fail
+        if t[i] == 0:
+            open_[int(p[i])] = i
+        elif int(p[i]) in open_:
+            if t[i] == 2:
+                fails.add(open_[int(p[i])])
+            del open_[int(p[i])]
+    live, best, pend = 0, 0, {}
     for i in range(len(t)):
         if t[i] == 0:
-            open_[int(p[i])] = True
+            if i in fails:
+                continue
+            pend[int(p[i])] = True
             live += 1
             best = max(best, live)
-        elif t[i] in (1, 2):  # :ok / :fail complete the process's open call
-            if open_.pop(int(p[i]), None):
-                live -= 1
+        elif t[i] == 1 and pend.pop(int(p[i]), None):
+            live -= 1
     return best
 
 
@@ -66,7 +76,7 @@ def cpu_leg(ops, clients, k, q):
            "max_frontier": int(r.get("max_frontier", -1))})
 
 
-def gpu_leg(ops, clients, k, part, q):
+def gpu_leg(ops, clients, k, part, part_cap, q):
     from lincheck import _lib
     h = make(ops, clients, k)
     out = {}
@@ -84,7 +94,7 @@ def gpu_leg(ops, clients, k, part, q):
     if part:
         t = time.perf_counter()
         try:
-            p = _lib.part_check(h, 0, 1)
+            p = _lib.part_check(h, 0, 1, part_cap)
             out["lc_part_check"] = {"wall_s": time.perf_counter() - t, "valid": int(p["valid"][0]),
                                     "explored": int(p["explored"][0]), "err": int(p["err"][0])}
         except Exception as e:  # capacity errors come back as :unknown; anything else is reported
@@ -122,6 +132,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--part", action="store_true")
+    ap.add_argument("--part-cap", type=int, default=0, help="lc_part_check capacity_log2 (0: default)")
     a = ap.parse_args()
     ks = [int(x) for x in a.crashed.split(",") if x]
     rows = {}
@@ -137,7 +148,7 @@ def main():
                 break
     if not a.no_gpu:
         for k in ks:
-            rows[k]["gpu"] = run_child(gpu_leg, (a.ops, a.clients, k, a.part), a.gpu_timeout)
+            rows[k]["gpu"] = run_child(gpu_leg, (a.ops, a.clients, k, a.part, a.part_cap), a.gpu_timeout)
             print(f"[ramp] K={k} gpu {rows[k]['gpu']}", file=sys.stderr, flush=True)
             if "timeout_s" in rows[k]["gpu"] or "error" in rows[k]["gpu"]:
                 break
