@@ -1354,6 +1354,10 @@ constexpr int MRING = DENSE_MRING;
 // super-layers after it was written, as before. Mirror slots: a step's words are read up to
 // H + T super-layers after its start, plus the 16-super-layer credit lag (MRING = 64).
 constexpr int PIPE_GLAY = 8192;
+constexpr int PIPE_XCD = 16384;  // XCD-compact workgroup roles in the big kernel (dense_big_kernel)
+// tile teams: credit tokens pre-polled a super-layer early (r3n A/B, 2 runs each: C2 30.08 ->
+// 29.92 ms, 8-way shares 0/1 7.14 -> 7.12 / 7.03 -> 6.97, C3 11.46 -> 11.44)
+constexpr int PIPE_CPRE = 65536;
 
 __device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
                                            unsigned long long need, uint64_t t0, long& spins) {
@@ -1429,21 +1433,35 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   }
   __syncthreads();
   int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0, last_start = 0;
+  // credit pre-poll: the decoder lanes load every tile's token one super-layer before a credit
+  // check (lane = tile, 64 tiles per register), so the check's first poll costs no HBM round
+  // trip when nobody lags (tokens only grow: an early value that suffices stays valid)
+  unsigned long long cpre[4] = {0, 0, 0, 0};
+  static_assert((1 << DENSE_TEAM_MAXB) <= 4 * 64, "credit pre-poll registers");
   for (int s = 0; t_ret < ns; ++s) {
     unsigned long long tp = timed ? now() : 0;
     if (s >= 8 && (s & 7) == 0) {  // credit: nobody more than 8 super-layers behind
       if (decoder) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         long spins = 0;
-        for (int r0 = 0; r0 < G; r0 += 64)  // one lane per tile, 64 tiles at a time
-          while (!__all(r0 + lane >= G ||
-                        poll_until(p, &flags[r0 + lane < G ? r0 + lane : 0], (unsigned long long)(s - 8), t0, spins)))
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // one lane per tile, 64 tiles at a time
+          const int r = 64 * k + lane;
+          if (64 * k >= G) break;
+          const bool pre_ok = r >= G || cpre[k] >= (unsigned long long)(s - 8);
+          while (!__all(pre_ok || poll_until(p, &flags[r < G ? r : 0], (unsigned long long)(s - 8), t0, spins)))
             ;
-        if (tid == 0) *sAbort = ld_agent(p.abort);
+        }
+        if (lane == 0) *sAbort = ld_agent(p.abort);
       }
       __syncthreads();
       if (*sAbort) break;
       if (timed) ph[3] += now() - tp, tp = now();
+    }
+    if (decoder && (p.pipe & PIPE_CPRE) && s >= 7 && (s & 7) == 7) {  // the next check's tokens, loaded now
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        cpre[k] = 64 * k + lane < G ? ld_agent(&flags[64 * k + lane]) : 0ull;
     }
     // ---- ring view: lane i = step t_ret + i
     const int tl = t_ret + lane;
@@ -1705,6 +1723,8 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     if (t_run < t_dec_old) {
       const int lp = t_run - 1 - t_ret_old;
       const int gap = (dbl && lp >= 0 && rdl(h1.x, lp) < 3) ? 1 : 2;  // as in history_pipe
+      // (r3n: a gap of 3 after team-slot returns, so that a tile's X is another tile's word of two
+      // super-layers back, cost more super-layers than it saved: C2 30.1 -> 31.0 ms)
       const bool ok = lp < 0 || lp < lead || s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h1.z, lp) + rdl(tb_l, lp) + 1);
       if (ok) {
         if (tid == 0) ring[t_run % RING].start = s + 1, ring[t_run % RING].pstart = last_start;
@@ -1719,7 +1739,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     if (timed) ph[2] += now() - tp, ph[5] += 1;
   }
   if (timed && tid == 0)
-    for (int k = 0; k < 6; ++k) p.tstamps[blockIdx.x * 8 + k] = ph[k];
+    for (int k = 0; k < 6; ++k) p.tstamps[(base + rank) * 8 + k] = ph[k];
   // make sure the last token is out before the team barrier's readers look (the barrier orders it)
   if (ns > 0) {  // the last step's return, over this tile, once every tile has finished
     team_bar((TeamCtl*)p.ctl + team, G, p.abort, sAbort);
@@ -1874,14 +1894,22 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   __syncthreads();
   unsigned long long st_fout = 0, st_steps = 0;
 
-  if ((int)blockIdx.x >= p.n_team_wgs) {  // ------------------------------- BLOCK histories
+  // LC_PIPE bit 14 (PIPE_XCD): workgroup roles by an XCD-compact index. Blocks are dealt
+  // round-robin over the 8 XCDs (MI355X_MICROARCH "Workgroup dispatch": b and b + 8 share one), so
+  // index (b % 8) * (grid / 8) + b / 8 puts consecutive team workgroups on one XCD: a team of <= 32
+  // tiles hands its mirror words off inside one XCD (handoff-1to1: cross-XCD +0.1-0.3 us). Speed
+  // only: the hand-off protocol (sc1 granules, tags) is the same under any placement.
+  const int bid = ((p.pipe & PIPE_XCD) && (gridDim.x & 7u) == 0)
+                      ? (int)((blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3))
+                      : (int)blockIdx.x;
+  if (bid >= p.n_team_wgs) {  // ------------------------------------------------ BLOCK histories
     // the last ceil(n_w / 16) workgroups start on the WAVE queue: a WAVE history is a long
     // latency-bound chain, and started after the BLOCK queue it would be the launch's tail
     const int wave_first = p.n_w > 0 ? (p.n_w + 15) / 16 : 0;
-    if (wave_first && (int)blockIdx.x >= (int)gridDim.x - wave_first)
+    if (wave_first && bid >= (int)gridDim.x - wave_first)
       big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     // and the next mid_first start on the MID queue (long chains too, four per workgroup)
-    else if (p.n2 > 0 && (p.pipe & 128) && (int)blockIdx.x >= (int)gridDim.x - wave_first - p.mid_first)
+    else if (p.n2 > 0 && (p.pipe & 128) && bid >= (int)gridDim.x - wave_first - p.mid_first)
       big_mid_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     if (p.pipe & 1) {
       history_pipe<1024, DENSE_LMAX, BLOCK_RING>(p, sTab, &sZero, sRing, &sQ, &sRed, p.words, sWOff, sBinom, tid,
@@ -1903,9 +1931,9 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   }
 
   // ------------------------------------------------------------------------- TILE team
-  const int team = p.wg_team[blockIdx.x];
+  const int team = p.wg_team[bid];
   const int base = p.team_base[team];
-  const int rank = (int)blockIdx.x - base;
+  const int rank = bid - base;
   const int G = 1 << p.team_bits[team];
   const int h = p.team_hist[team];
   TeamCtl* const ctl = (TeamCtl*)p.ctl + team;
@@ -2237,7 +2265,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
     if (tid == 0 && e) atomicAdd(&p.explored[h], e);
   }
   if (p.tstamps && tid == 0)
-    for (int i = 0; i < 6; ++i) p.tstamps[blockIdx.x * 8 + i] = ph[i];
+    for (int i = 0; i < 6; ++i) p.tstamps[(base + rank) * 8 + i] = ph[i];
   if (nobar && (p.pipe & 1)) {
     // the team is done (its final barrier passed, and other tiles read only this tile's HBM
     // mirror, never its LDS): join the BLOCK queue, whose heaviest-first order leaves the

@@ -208,9 +208,10 @@ struct lc_plan {
   // fixpoint for steps of at most 7 slots (r3d A/B, 3 runs each: C1 0.523 -> 0.428 ms, C3 11.57
   // -> 11.59 ms); bit 12 = X of a step after a hi return from its inputs (off); bit 13 = tile
   // teams on global popcount layers (off); bit 14 = XCD-compact workgroup roles in the big
-  // kernel (r3l A/B, 2 runs each: C3 11.64 -> 11.55 ms, C2 and 8-way shares unchanged).
-  // Default 20431 = 1|2|4|8|64|128|256|512|1024|2048|16384, with the planner.
-  int dense_pipe = 20431;
+  // kernel (r3l A/B, 2 runs each: C3 11.64 -> 11.55 ms, C2 and 8-way shares unchanged); bit 16 =
+  // tile teams pre-poll their credit tokens a super-layer early (r3n: -0.5 to -1 %).
+  // Default 85967 = 1|2|4|8|64|128|256|512|1024|2048|16384|65536, with the planner.
+  int dense_pipe = 85967;
   bool pipe_env = false;  // LC_PIPE given: its bits as they are
   std::vector<int> plan_lb;  // team planner: local slots per tile (0: not a team)
   bool plan_off = false;     // LC_TEAM_PLAN=0: every wide history keeps 17-bit tiles
@@ -351,6 +352,8 @@ struct lc_plan {
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
     if ((e = getenv("LC_PLAN_K")) && atof(e) > 0) plan_k16 = atof(e);
     if ((e = getenv("LC_PLAN_X")) && atof(e) > 0) plan_x = atof(e);
+    if ((e = getenv("LC_PLAN_KB")) && atof(e) > 0) plan_kb = atof(e);
+    if ((e = getenv("LC_PLAN_ROT"))) plan_rot = atoi(e) != 0;
     if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
     if ((e = getenv("LC_TEAM_ROT_LB"))) rot_min_lb = atoi(e);
     if ((e = getenv("LC_TEAM_ROT_CHAIN"))) rot_chain_lb = atoi(e);
@@ -377,8 +380,8 @@ struct lc_plan {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_from = 99, wide_lbits = DENSE_LMAX;
-    dense_pipe = 20431, pipe_env = false, plan_off = false;
-    plan_k16 = -1, plan_x = 1.57, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
+    dense_pipe = 85967, pipe_env = false, plan_off = false;
+    plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
     rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
     kfcap = klcap = 1 << 18;
     cell_cap = 256;
@@ -620,17 +623,12 @@ struct lc_plan {
     if (team_rot != 0)
       for (int h : dense_x) {
         const int lw = enc.live_max[h], lb = team_lbits(h);
-        if (team_rot < 0) {  // auto: a batch plan's big-tile teams, or mostly-wide histories
-          int wide = 0;
-          for (int L = lb + 1; L <= 32; ++L) wide += (int)widths[h].c[L];
-          const bool mostly_wide = 10 * wide >= 4 * (int)widths[h].steps();
-          // a chain plan's widest teams (14-slot tiles, >= 4 team bits: 16+ tiles) gain from it
-          // too (r3i, every 8-way C3 share rotated and not: w21/lb14 8.46 -> 7.37 ms and 6.64 ->
-          // 6.22, w18/lb14 6.24 -> 5.91; w17/lb14 (3 team bits) 6.62 -> 6.86, and 13-slot tiles
-          // lose at every width: w19/lb13 6.39 -> 7.08, w20/lb13 6.34 -> 7.05)
-          const bool chain_widest = !batch_plan() && lb == rot_chain_lb && lw - lb >= 4;
-          if (!chain_widest && (lb < rot_min_lb || !(batch_plan() || mostly_wide))) continue;
-        }
+        // auto (will_rotate): a batch plan's big-tile teams, or mostly-wide histories, and a
+        // chain plan's widest teams (14-slot tiles, >= 4 team bits: 16+ tiles), which gain from it
+        // too (r3i, every 8-way C3 share rotated and not: w21/lb14 8.46 -> 7.37 ms and 6.64 ->
+        // 6.22, w18/lb14 6.24 -> 5.91; w17/lb14 (3 team bits) 6.62 -> 6.86, and 13-slot tiles
+        // lose at every width: w19/lb13 6.39 -> 7.08, w20/lb13 6.34 -> 7.05)
+        if (team_rot < 0 && !will_rotate(widths[h], lw, lb)) continue;
         const int r = team_rot < 0 ? lw - lb : std::min(team_rot, lw - lb);
         if (r <= 0) continue;
         // with the encoder's slot policy the in-word slots 0..2 hold the soonest-returning ops:
@@ -739,19 +737,38 @@ struct lc_plan {
   // chain and keeps a higher factor (C2: 0.7 -> 35.5 ms, 0.4 -> 39.1 ms; rank shares: 1.0, r2cd).
   double plan_k16 = -1;  // < 0: 0.45 for a batch plan, else 1.0 (r2cd)
   double plan_x = 1.57;  // LC_PLAN_X: the team model's cost per team bit (us per step)
+  double plan_kb = 0.45;  // LC_PLAN_KB: the batch plan's VALU factor
+  bool plan_rot = false;  // LC_PLAN_ROT: the team model knows which teams will be rotated
   // A batch plan (LC_BATCH_HIST: more than 600 histories, e.g. C3 on one GPU) fills the chip,
   // so the launch is throughput-bound; fewer histories leave workgroups idle and the launch is
   // its slowest chain (r2rot6-8: C3 1000 keys 11.8 ms batch / 16.2 unrotated; a 250-key share
   // 8.2-9.5 ms as a chain plan, 9.6-9.9 as a batch plan).
   int batch_hist = 600;  // (r2bh: a 500-key share as a chain plan: slowest rank 11.3 -> 10.9 ms)
   bool batch_plan() const { return enc.n_hist > batch_hist; }
-  double est_team_us(const WidthHist& ws, int lb) const {
-    const double k = plan_k16 > 0 ? plan_k16 : batch_plan() ? 0.45 : 1.0;
+  // Will build_dense rotate history h's team of lb-slot tiles? (the rule documented there)
+  bool will_rotate(const WidthHist& ws, int lw, int lb) const {
+    if (team_rot == 0 || lw <= lb) return false;
+    if (team_rot > 0) return true;
+    int wide = 0;
+    for (int L = lb + 1; L <= 32; ++L) wide += (int)ws.c[L];
+    const bool mostly_wide = 10 * wide >= 4 * (int)ws.steps();
+    const bool chain_widest = !batch_plan() && lb == rot_chain_lb && lw - lb >= 4;
+    return chain_widest || (lb >= rot_min_lb && (batch_plan() || mostly_wide));
+  }
+  // lw: the history's widest step. A rotated team (LC_PLAN_ROT, r3) has its t = lw - lb team
+  // bits among the slots live in almost every step: every step is spread over the tiles (local
+  // width L - t) and pays the exchange; unrotated, a step of width L <= lb runs on tile 0 alone.
+  double est_team_us(const WidthHist& ws, int lb, int lw = 0) const {
+    const double k = plan_k16 > 0 ? plan_k16 : batch_plan() ? plan_kb : 1.0;
+    const bool rot = plan_rot && lw > lb && will_rotate(ws, lw, lb);
+    const int tb = rot ? lw - lb : 0;
     double t = 0;
     for (int L = 0; L <= 32; ++L) {
       if (!ws.c[L]) continue;
-      double u = 1.59 + 0.0043 * k * std::ldexp(1.0, std::max(0, std::min<int>(L, lb) - 3));
-      if (L > lb) u += 3.87 + plan_x * (L - lb);
+      const int Lloc = rot ? std::max(3, L - tb) : std::min<int>(L, lb);
+      double u = 1.59 + 0.0043 * k * std::ldexp(1.0, std::max(0, std::min(Lloc, lb) - 3));
+      if (rot) u += 3.87 + plan_x * tb;
+      else if (L > lb) u += 3.87 + plan_x * (L - lb);
       t += ws.c[L] * u;
     }
     return t;
@@ -766,7 +783,7 @@ struct lc_plan {
     std::vector<double> est(enc.n_hist, 0.0);
     std::vector<char> in_block(enc.n_hist, 0);
     int team_wgs = 0;
-    for (int h : dense_x) team_wgs += wgs(h, DENSE_LMAX), est[h] = est_team_us(ws[h], DENSE_LMAX);
+    for (int h : dense_x) team_wgs += wgs(h, DENSE_LMAX), est[h] = est_team_us(ws[h], DENSE_LMAX, enc.live_max[h]);
     double pool = 0;
     for (int h : dense_b) in_block[h] = 1, est[h] = est_block_us(ws[h]), pool += est[h];
     if (dense_pipe & 64)  // WAVE histories on the big kernel's waves, 16 per workgroup
@@ -791,7 +808,7 @@ struct lc_plan {
       for (int lb = cur - 1; lb >= 13 && lw - lb <= maxb; --lb) {
         const int x = wgs(best, lb) - (in_block[best] ? 1 : wgs(best, cur));
         if (team_wgs + x > cap || dgrid_b - team_wgs - x < 1) break;
-        const double t = est_team_us(ws[best], lb);
+        const double t = est_team_us(ws[best], lb, lw);
         const double pool_new = (pool - (in_block[best] ? est[best] : 0.0)) / (dgrid_b - team_wgs - x);
         const double m = std::max(std::max(t, second), pool_new);
         if (m < m_best - 1.0) nlb = lb, extra = x, t_new = t, m_best = m;
