@@ -23,6 +23,7 @@
 #include "../../include/lincheck.h"
 #include "bounds.hpp"
 #include "dense.hpp"
+#include "wide.hpp"
 #include "encode.hpp"
 #include "keys.hpp"
 #include "pool.hpp"
@@ -162,6 +163,12 @@ struct lc_plan {
   // dense closure tables (narrow cas-register histories; dense.hpp)
   std::vector<int> dense_b, dense_w, dense_x, dense_m;  // block / wave / wide / mid teams, heaviest first
   DevArray d_dpack, d_dwords, d_dqueue, d_dstatus, d_dfail, d_dexpl;
+  // histories wider than the LDS tile teams hold: tables in HBM (wide.hip)
+  std::vector<int> dense_wd;
+  std::vector<char> wide_ok;
+  std::vector<std::vector<uint32_t>> wide_streams;  // per history (built by dense_sink)
+  DevArray d_wtab, d_wstream, d_wmeta, d_wres, d_wbar;
+  int wide_maxw = WIDE_LMAX, wide_minw = 0;  // LC_WIDE_MAXW (0: off) / LC_WIDE_MINW (tests)
   // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
   // begin / step count / table width, and the queue order
   uint32_t* dp_stream = nullptr;
@@ -347,6 +354,8 @@ struct lc_plan {
     // dense-path knobs (tests): workgroups tile teams may take per launch, widest history
     if ((e = getenv("LC_TILE_WGS")) && atoi(e) > 0) tile_cap = atoi(e);
     if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
+    if ((e = getenv("LC_WIDE_MAXW"))) wide_maxw = std::max(0, std::min(atoi(e), WIDE_LMAX));
+    if ((e = getenv("LC_WIDE_MINW"))) wide_minw = std::max(0, atoi(e));
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e), pipe_env = true;
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
@@ -379,6 +388,7 @@ struct lc_plan {
   void reset_knobs() {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
+    wide_maxw = WIDE_LMAX, wide_minw = 0;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 85967, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
@@ -506,9 +516,12 @@ struct lc_plan {
     dense_w.clear();
     dense_x.clear();
     dense_m.clear();
+    dense_wd.clear();
     dense_on = model == LC_MODEL_CAS_REGISTER && path == 0 && dgrid_b > 0 && dgrid_w > 0 && dgrid_m > 0;
     if (!dense_on) return 0;
     dense_ok.assign(n, 0);
+    wide_ok.assign(n, 0);
+    if ((int)wide_streams.size() < n) wide_streams.resize(n);
     dense_cost.assign(n, 0.0);
     dense_nw.assign(n, 0);
     widths.resize(n);
@@ -545,9 +558,16 @@ struct lc_plan {
     dalg_tot[h] = StepBytes{0, 0};
     nst[h] = 0;
     lm[h] = 0;
-    bool ok = !v.err && v.n_states <= DENSE_MAX_STATES && v.live_max <= dense_maxw;
+    bool ok = !v.err && v.n_states <= DENSE_MAX_STATES;
     for (int64_t t = 0; t < v.n_steps && ok; ++t)  // a step's words must fit the decoders' window
       if (v.step_ninv[t] > DENSE_MAX_NINV) ok = false;
+    // wider than the LDS tile teams hold (or from LC_WIDE_MINW on, tests): tables in HBM
+    const int wmin = wide_minw > 0 ? wide_minw : dense_maxw + 1;
+    if (ok && v.live_max >= wmin && v.live_max <= wide_maxw) {
+      wide_sink(h, v);
+      return false;  // (its invocation arrays stay: lc_failure_configs re-runs it on the grid kernel)
+    }
+    ok = ok && v.live_max <= dense_maxw;
     dense_ok[h] = ok;
     if (!ok) return false;
     nst[h] = (int32_t)v.n_steps;
@@ -585,6 +605,32 @@ struct lc_plan {
     return !keep_inv_arrays;
   }
 
+  // A wide history's step stream (wide.hpp: two header words, then its op words), into its own
+  // buffer: wide histories are rare, and the upper-bound layout of the others has no room for
+  // the second header word.
+  void wide_sink(int h, const HistView& v) {
+    std::vector<uint32_t>& out = wide_streams[h];
+    out.clear();
+    uint32_t live = 0;
+    int64_t q = 0;
+    for (int64_t t = 0; t < v.n_steps; ++t) {
+      if (t > 0) live &= ~(1u << v.step_slot[t - 1]);
+      const int64_t q1 = q + v.step_ninv[t];
+      for (int64_t k = q; k < q1; ++k) live |= 1u << v.inv_slot[k];
+      out.push_back(live);
+      out.push_back((uint32_t)v.step_slot[t]);
+      for (int64_t k = q; k < q1; ++k) {
+        const int64_t a = v.inv_a[k], b = v.inv_b[k];
+        const uint32_t am = a == R_ANY ? 0xffu : (a == R_NEVER ? 0u : (1u << a));
+        const uint32_t bm = b < 0 ? 0u : (1u << b);
+        out.push_back((uint32_t)v.inv_slot[k] | (am << 8) | (bm << 16) | DENSE_OPW);
+      }
+      q = q1;
+    }
+    out.push_back(0u);
+    wide_ok[h] = 1;
+  }
+
   int build_dense() {
     const auto t_build = std::chrono::steady_clock::now();
     auto ms_since_build = [&] {
@@ -599,6 +645,8 @@ struct lc_plan {
     int32_t* const ordp = (int32_t*)(hpack + o_ord);
     const double t_fill = ms_since_build();
     up_ptr = nullptr;  // (a new layout: upload the team tables again)
+    for (int h = 0; h < n; ++h)
+      if (wide_ok[h]) dense_wd.push_back(h);
     for (int h = 0; h < n; ++h) {
       if (!ok[h]) continue;
       const int lw = enc.live_max[h];
@@ -1507,6 +1555,122 @@ struct lc_plan {
     return free_b;
   }
 
+  // The wide histories (tables in HBM), one persistent launch over the whole GPU, one history
+  // after another. `ran` stays false when the two tables do not fit the device (they then take
+  // the grid kernel, as before).
+  int run_wide(float* ms, bool& ran) {
+    const int nwd = (int)dense_wd.size();
+    std::vector<int64_t> sbeg(nwd);
+    std::vector<int32_t> nst(nwd);
+    std::vector<int8_t> lmx(nwd);
+    std::vector<uint32_t> words;
+    int lmax = 0;
+    for (int i = 0; i < nwd; ++i) {
+      const int h = dense_wd[i];
+      sbeg[i] = (int64_t)words.size();
+      nst[i] = enc.n_steps(h);
+      lmx[i] = (int8_t)enc.live_max[h];
+      lmax = std::max(lmax, (int)enc.live_max[h]);
+      words.insert(words.end(), wide_streams[h].begin(), wide_streams[h].end());
+    }
+    words.resize(words.size() + 64, 0u);  // the decoders read a 64-word window
+    const int64_t tw = (int64_t)1 << std::max(0, lmax - 3);
+    if (d_wtab.ensure((size_t)tw * 16) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    int rc;
+    if ((rc = upload(d_wstream, words))) return rc;
+    if (!d_dwords.p) {
+      std::vector<uint32_t> wl(1u << DENSE_WORD_BITS);
+      dense_word_list(DENSE_WORD_BITS, wl.data());
+      if ((rc = upload(d_dwords, wl))) return rc;
+    }
+    // meta: sbeg | nsteps | lmax; results: explored | any | status | fail | stats[2]
+    const size_t m_sb = (size_t)nwd * 8, m_ns = (size_t)nwd * 4;
+    HIP_TRY(d_wmeta.ensure(m_sb + m_ns + (size_t)nwd + 8));
+    HIP_TRY(hipMemcpy(d_wmeta.p, sbeg.data(), m_sb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((char*)d_wmeta.p + m_sb, nst.data(), m_ns, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((char*)d_wmeta.p + m_sb + m_ns, lmx.data(), (size_t)nwd, hipMemcpyHostToDevice));
+    const size_t r_bytes = (size_t)nwd * 24 + 16;
+    HIP_TRY(d_wres.ensure(r_bytes));
+    HIP_TRY(d_wbar.ensure(wide_bar_bytes() + 8));
+    HIP_TRY(hipMemsetAsync(d_wres.p, 0, r_bytes, stream));
+    HIP_TRY(hipMemsetAsync(d_wbar.p, 0, wide_bar_bytes() + 8, stream));
+    WideParams p{};
+    p.n = nwd;
+    p.sbeg = (const int64_t*)d_wmeta.p;
+    p.nsteps = (const int32_t*)((char*)d_wmeta.p + m_sb);
+    p.lmax = (const int8_t*)((char*)d_wmeta.p + m_sb + m_ns);
+    p.stream = d_wstream.as<uint32_t>();
+    p.words = d_dwords.as<uint32_t>();
+    p.tab = d_wtab.as<uint64_t>();
+    p.tab_words = tw;
+    unsigned long long* const rex = d_wres.as<unsigned long long>();
+    p.explored = rex;
+    p.any = rex + nwd;
+    p.status = (int32_t*)(rex + 2 * nwd);
+    p.fail_step = p.status + nwd;
+    p.stats = (unsigned long long*)(p.fail_step + nwd);
+    p.bar = d_wbar.as<unsigned>();
+    p.abort = (int32_t*)((char*)d_wbar.p + wide_bar_bytes());
+    const int grid = wide_grid_size();
+    if (grid < 1) {
+      last_error = "wide kernel: no resident workgroups";
+      return LC_E_INTERNAL;
+    }
+    HIP_TRY(hipEventRecord(ev0, stream));
+    HIP_TRY(launch_wide(p, grid, stream));
+    HIP_TRY(hipEventRecord(ev1, stream));
+    std::vector<unsigned long long> res((r_bytes + 7) / 8);
+    int32_t ab = 0;
+    HIP_TRY(hipMemcpyAsync(res.data(), d_wres.p, r_bytes, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(&ab, p.abort, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
+    *ms += t;
+    if (ab) {
+      last_error = "wide kernel: grid barrier watchdog fired";
+      return LC_E_INTERNAL;
+    }
+    const int32_t* st = (const int32_t*)(res.data() + 2 * nwd);
+    const int32_t* fs = st + nwd;
+    const unsigned long long* ss = (const unsigned long long*)(fs + nwd);
+    for (int i = 0; i < nwd; ++i) {
+      const int h = dense_wd[i];
+      status[h] = st[i], fail_step[h] = fs[i], explored[h] = res[i];
+    }
+    stats[1] += 1;
+    stats[2] += (double)ss[1];
+    stats[12] += nwd;  // (dense histories: LDS or HBM tables)
+    stats[13] += t;
+    stats[31] += nwd;
+    stats[32] += t;
+    // algorithmic bytes: every live word of every step read as X, pulled by its popcount-q
+    // successors... counted from the reader: X (8 B) + popcount pulls (8 B each) + its store
+    double alg = 0;
+    for (int i = 0; i < nwd; ++i) {
+      const int h = dense_wd[i];
+      const std::vector<uint32_t>& ws = wide_streams[h];
+      const int fs_i = fs[i];
+      size_t q = 0;
+      for (int tt = 0; tt < enc.n_steps(h) && q + 1 < ws.size(); ++tt) {
+        if (fs_i >= 0 && tt > fs_i + 1) break;
+        const int n = __builtin_popcount(ws[q] >> 3);
+        alg += std::ldexp(1.0, n) * (n / 2.0 + 2.0) * 8.0;
+        q += 2;
+        while (q < ws.size() && (ws[q] & DENSE_OPW)) ++q;
+      }
+    }
+    stats[33] += alg;
+    if (debug())
+      fprintf(stderr, "[lincheck] wide: %d histories (tables of 2^%d words in HBM), %.3f ms, steps=%llu Fout=%llu\n",
+              nwd, std::max(0, lmax - 3), t, ss[1], ss[0]);
+    ran = true;
+    return 0;
+  }
+
   int run_grid(const std::vector<int>& ids, float* ms) {
     make_batches(ids);
     for (size_t bi = 0; bi < batches.size(); ++bi) {
@@ -1565,6 +1729,12 @@ struct lc_plan {
       for (int h : dense_w) done[h] = 1;
       for (int h : dense_x) done[h] = 1;
       for (int h : dense_m) done[h] = 1;
+    }
+    if (max_t == INT32_MAX && path == 0 && dense_on && !dense_wd.empty()) {
+      bool ran = false;
+      if ((rc = run_wide(&ms, ran))) return rc;
+      if (ran)
+        for (int h : dense_wd) done[h] = 1;
     }
     if (keys) {
       if ((rc = upload_grid())) return rc;

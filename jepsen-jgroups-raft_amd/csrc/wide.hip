@@ -1,0 +1,289 @@
+// wide.hip — the closure-table search with its tables in HBM (wide.hpp), for
+// cas-register histories of live width DENSE_WIDE_LMAX < L <= WIDE_LMAX: knossos.linear/analysis
+// [ext] with CASRegister.step (a6) on whole byte-sliced words, as dense.hip,
+// bit-exact with it and with the oracle.
+//
+// One persistent launch runs the wide histories one after another; all workgroups work on the
+// same history. RETURN step t (its table T_t = tab(t & 1), the previous step's T_{t-1} intact):
+//   for q = 0..H:  every word w of popcount q with w within the live hi slots, spread over the
+//                  whole grid: X = T_{t-1} read through the previous return (pipe_x), the pulls
+//                  T_t[w \ b] over w's set bits, the in-word closure; T_t[w] = X | R
+//                  grid barrier
+// so the DP is dense.hip's run_layers with the layers as grid-wide phases. A layer's words are
+// (high part a, low part from the sorted word list): w = a << k | low, k = min(H, 19), the
+// 2^(H-k) <= 256 high parts in a per-layer prefix table (LDS), so a thread's word comes from a
+// binary search over <= 8 entries and one list load, and consecutive threads take consecutive
+// low words of one high part (neighbouring table words).
+// Failure: each step ORs "some X was nonzero" (step t-1's post-return frontier held a config)
+// into `any` as an atomicMax of t + 1 before its last barrier; after it every workgroup reads
+// the same value, so all leave together (an empty frontier stays empty).
+#include "dense.hpp"
+#include "dense_ops.hpp"
+#include "device_common.hpp"
+#include "search.hpp"
+#include "wide.hpp"
+
+namespace lc {
+namespace {
+
+constexpr int WWG = 1024;
+constexpr int WB = 32;  // binomials C(n, k) for n < 32 (u32: C(31, 15) = 300,540,195)
+constexpr int WH = WIDE_LMAX - 3;  // most hi bits
+constexpr int WPRE = 257;          // per layer: prefix over <= 256 high parts, + the total
+
+struct WideBar {  // two-level arrival counters + generation, each on its own 128-B lines
+  unsigned grp[8][32];
+  unsigned top;
+  unsigned pad0[31];
+  unsigned gen;
+  unsigned pad1[31];
+};
+
+// Grid barrier (search.hip's grid_sync without fences): every wave drains its sc1 stores, one
+// lane per workgroup arrives on its group's counter, the last of a group on the top counter,
+// the last of those bumps the generation the others poll (relaxed loads, s_sleep); 20 s
+// without a release raises *abort. The table words are sc1 stores read with sc1 loads.
+__device__ __forceinline__ bool wide_sync(const WideParams& p, int* sAbort) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    WideBar* bar = reinterpret_cast<WideBar*>(p.bar);
+    const unsigned nwg = gridDim.x;
+    const unsigned g = ld_agent(&bar->gen);
+    const unsigned grp = blockIdx.x & 7u;
+    const unsigned gsize = (nwg - grp + 7u) >> 3;
+    const unsigned ngroups = nwg < 8u ? nwg : 8u;
+    if (__hip_atomic_fetch_add(&bar->grp[grp][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      st_agent(&bar->grp[grp][0], 0u);
+      if (__hip_atomic_fetch_add(&bar->top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1) {
+        st_agent(&bar->top, 0u);
+        __hip_atomic_store(&bar->gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    long spins = 0;
+    while (ld_agent(&bar->gen) == g) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+          st_agent(p.abort, 1);
+          break;
+        }
+        if (ld_agent(p.abort)) break;
+      }
+    }
+    *sAbort = ld_agent(p.abort);
+  }
+  __syncthreads();
+  return *sAbort == 0;
+}
+
+// pulls of word w from T_t over its set bits (only j's when it holds j), eight loads in flight
+// per round: the loads are independent, so a round costs one HBM round trip
+__device__ __forceinline__ uint64_t wide_pulls(const uint64_t* B, uint32_t w, uint32_t jh, const OpSel* ops,
+                                              uint32_t foldm) {
+  uint32_t m = (w & jh) ? jh : w;
+  uint64_t R = 0;
+  while (m) {
+    int bb[8];
+    uint64_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      bb[u] = m ? __builtin_ctz(m) : -1;
+      m &= m - 1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = bb[u] >= 0 ? HbmTab::ld(&B[w ^ (1u << bb[u])]) : 0ull;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (bb[u] >= 0) R |= transfer(ops[bb[u] + 3], (foldm >> (bb[u] + 3)) & 1u, v[u]);
+  }
+  return R;
+}
+
+__global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
+  __shared__ uint32_t sBin[WB * WB];
+  __shared__ uint32_t sPre[(WH + 1) * WPRE];
+  __shared__ uint32_t sLay[WIDE_LOW_BITS + 2];  // first entry of each popcount layer of the list
+  __shared__ OpSel sOps[32];                     // slot k's op
+  __shared__ uint32_t sHdr[4];                   // live, j, fresh, foldm
+  __shared__ unsigned long long sRed;
+  __shared__ int sAbort;
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < WB * WB; i += WWG) {
+    const int n = i / WB, k = i % WB;
+    uint64_t c = 0;
+    if (k <= n) {
+      c = 1;
+      for (int q = 1; q <= k; ++q) c = c * (uint64_t)(n - k + q) / (uint64_t)q;
+    }
+    sBin[i] = (uint32_t)c;
+  }
+  if (tid == 0) sAbort = 0;
+  __syncthreads();
+  if (tid <= WIDE_LOW_BITS + 1) {
+    uint32_t o = 0;
+    for (int r = 0; r < tid; ++r) o += sBin[DENSE_WORD_BITS * WB + r];
+    sLay[tid] = o;
+  }
+  const int64_t gtid = (int64_t)blockIdx.x * WWG + tid, gstride = (int64_t)gridDim.x * WWG;
+  unsigned long long st_fout = 0, st_steps = 0;
+  for (int i = 0; i < p.n; ++i) {
+    const int ns = p.nsteps[i];
+    uint64_t* const T0 = p.tab;
+    uint64_t* const T1 = p.tab + p.tab_words;
+    auto tab = [&](int t) { return (t & 1) ? T1 : T0; };
+    // step 0 reads its frontier from tab(-1) = T1, at word 0 only (every slot is fresh there):
+    // the initial config (register nil = state 0, nothing linearized)
+    if (blockIdx.x == 0 && tid == 0) HbmTab::st(&T1[0], 1ull);
+    if (tid < 32) sOps[tid] = OpSel{SEL_NONE, SEL_NONE};
+    if (!wide_sync(p, &sAbort)) break;
+    unsigned long long expl = 0;
+    int fail_t = -1, cH = -1, pj = -1;
+    uint32_t plive = 0;
+    int64_t pos = p.sbeg[i];
+    for (int t = 0; t < ns; ++t) {
+      // ---- decode (wave 0 of every workgroup): 2 header words, then the op words
+      if (tid < 64) {
+        const uint32_t wd = p.stream[pos + lane];
+        const uint32_t live = (uint32_t)__shfl((int)wd, 0, 64), j = (uint32_t)__shfl((int)wd, 1, 64);
+        const unsigned long long ob = __ballot(lane >= 2 && lane < 2 + DENSE_MAX_NINV && (wd & DENSE_OPW));
+        const int ninv = (int)__builtin_ctzll(~(ob >> 2));
+        if (lane >= 2 && lane < 2 + ninv) sOps[wd & 31u] = decode_op((wd >> 8) & 0xffu, (wd >> 16) & 0xffu);
+        // (after the stores: one wave's LDS ops stay in order)
+        const uint32_t foldm = (uint32_t)__ballot(lane < 32 && sOps[lane & 31].hi == OPS_FOLD);
+        if (lane == 0) {
+          sHdr[0] = live;
+          sHdr[1] = j;
+          sHdr[2] = t > 0 ? live & ~(plive & ~(1u << pj)) : live;  // slots invoked since the last return
+          sHdr[3] = foldm;
+        }
+        pos += 2 + ninv;
+      }
+      __syncthreads();
+      const uint32_t live = sHdr[0], fresh = sHdr[2], foldm = sHdr[3];
+      const int j = (int)sHdr[1], jp = pj;
+      const int L = 32 - __clz((int)live);
+      const int H = L > 3 ? L - 3 : 0;
+      const int k = H < WIDE_LOW_BITS ? H : WIDE_LOW_BITS, hb = H - k;
+      if (H != cH) {  // layer q's prefix over the high parts: sPre[q][a] = sum_{a' < a} C(k, q - |a'|)
+        if (tid <= H) {
+          uint32_t acc = 0;
+          for (int a = 0; a < (1 << hb); ++a) {
+            sPre[tid * WPRE + a] = acc;
+            const int r = tid - __popc(a);
+            if (r >= 0 && r <= k) acc += sBin[k * WB + r];
+          }
+          sPre[tid * WPRE + (1 << hb)] = acc;
+        }
+        cH = H;
+        __syncthreads();
+      }
+      const uint32_t live_hi = live >> 3, fresh_hi = fresh >> 3;
+      const uint32_t jh = j >= 3 ? 1u << (j - 3) : 0u;
+      uint64_t keep_lo = ~0ull;
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk)
+        if (fresh & (1u << kk)) keep_lo &= keep64(kk);
+      uint64_t* const B = tab(t);
+      const uint64_t* const Bp = tab(t - 1);
+      uint64_t anyx = 0;
+      bool ok = true;
+      for (int q = 0; q <= H && ok; ++q) {
+        const uint32_t* pre = &sPre[q * WPRE];
+        const uint32_t N = pre[1 << hb];
+        for (int64_t g = gtid; g < (int64_t)N; g += gstride) {
+          uint32_t a = 0;  // the last high part whose prefix is <= g (it holds g: its count > 0)
+          for (int bit = hb - 1; bit >= 0; --bit)
+            if (pre[a | (1u << bit)] <= (uint32_t)g) a |= 1u << bit;
+          const int r = q - __popc(a);
+          const uint32_t w = (a << k) | p.words[sLay[r] + ((uint32_t)g - pre[a])];
+          if (w & ~live_hi) continue;
+          uint64_t X = 0;
+          if (!(w & fresh_hi)) {  // the previous step's post-return table, read through its slot jp
+            if (jp >= 3) X = HbmTab::ld(&Bp[w | (1u << (jp - 3))]);
+            else if (jp >= 0) X = (HbmTab::ld(&Bp[w]) & ~keep64(jp)) >> (1 << jp);
+            else X = HbmTab::ld(&Bp[w]);
+            X &= keep_lo;
+          }
+          uint64_t R = wide_pulls(B, w, jh, sOps, foldm);
+          R = close_in_word(X, w, live, j, sOps, foldm, R);
+          HbmTab::st(&B[w], X | R);
+          expl += (uint64_t)__popcll(R);
+          if (t > 0) st_fout += (uint64_t)__popcll(X);
+          anyx |= X;
+        }
+        if (q == H && __any(anyx != 0) && lane == 0)  // step t-1's post-return frontier held a config
+          __hip_atomic_fetch_max(&p.any[i], (unsigned long long)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = wide_sync(p, &sAbort);
+      }
+      if (!ok) break;
+      ++st_steps;
+      plive = live, pj = j;
+      if (t > 0 && ld_agent(&p.any[i]) < (unsigned long long)(t + 1)) {  // the same value in every workgroup
+        fail_t = t - 1;
+        break;
+      }
+    }
+    if (sAbort) break;
+    if (fail_t < 0 && ns > 0) {  // the last step's return: its frontier must hold a config
+      const uint32_t lv = plive & ~(1u << pj);
+      const int Lf = lv ? 32 - __clz((int)lv) : 0;
+      const int64_t nwt = (int64_t)1 << (Lf > 3 ? Lf - 3 : 0);
+      const uint64_t* const Bl = tab(ns - 1);
+      uint64_t nz = 0;
+      for (int64_t w = gtid; w < nwt; w += gstride) {
+        if ((uint32_t)w & ~(lv >> 3)) continue;
+        uint64_t X;
+        if (pj >= 3) X = HbmTab::ld(&Bl[(uint32_t)w | (1u << (pj - 3))]);
+        else X = (HbmTab::ld(&Bl[w]) & ~keep64(pj)) >> (1 << pj);
+        st_fout += (uint64_t)__popcll(X);
+        nz |= X;
+      }
+      if (__any(nz != 0) && lane == 0)
+        __hip_atomic_fetch_max(&p.any[i], (unsigned long long)(ns + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!wide_sync(p, &sAbort)) break;
+      if (ld_agent(&p.any[i]) < (unsigned long long)(ns + 1)) fail_t = ns - 1;
+    }
+    // explored: one add per workgroup
+    for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
+    if (tid == 0) sRed = 0;
+    __syncthreads();
+    if (lane == 0 && expl) atomicAdd(&sRed, expl);
+    __syncthreads();
+    if (tid == 0) {
+      if (sRed) atomicAdd(&p.explored[i], sRed);
+      if (blockIdx.x == 0) {
+        p.status[i] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+        p.fail_step[i] = fail_t;
+      }
+    }
+    // (the next history's first store is to T1[0]: every workgroup is past this one's reads)
+    if (!wide_sync(p, &sAbort)) break;
+  }
+  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
+  if (lane == 0 && st_fout) atomicAdd(&p.stats[0], st_fout);
+  if (blockIdx.x == 0 && tid == 0 && st_steps) atomicAdd(&p.stats[1], st_steps);
+}
+
+}  // namespace
+
+int wide_grid_size() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel, WWG, 0) != hipSuccess || per_cu < 1) return 0;
+  return prop.multiProcessorCount;  // one workgroup per CU: every workgroup resident
+}
+
+size_t wide_bar_bytes() { return sizeof(WideBar); }
+
+hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream) {
+  WideParams q = p;
+  void* args[] = {&q};
+  return hipLaunchCooperativeKernel((const void*)wide_kernel, dim3(grid), dim3(WWG), args, 0, stream);
+}
+
+}  // namespace lc

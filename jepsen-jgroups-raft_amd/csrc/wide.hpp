@@ -1,0 +1,48 @@
+// wide.hpp — closure tables in HBM for cas-register histories wider than the LDS tile teams
+// hold: live width DENSE_WIDE_LMAX < L <= WIDE_LMAX.
+//
+// The same table and the same subset DP as dense.hpp (byte-sliced u64 words, one word per 8
+// masks; a RETURN step is its popcount layers in order), but the two tables (step t on t & 1)
+// live in HBM and the whole GPU works on one history: one persistent launch, every workgroup
+// takes a share of each popcount layer, a grid barrier ends the layer. Words are written with
+// sc1 (write-through) stores and read with sc1 (L1-bypassing) loads, so the barrier needs no
+// fences (the search kernel's level-phase protocol, MI355X_MICROARCH "Valid forms" row 1).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace lc {
+
+constexpr int WIDE_LMAX = 30;       // widest history: 2 tables of 2^27 words (2 GiB)
+constexpr int WIDE_LOW_BITS = 19;   // a layer's words = high part x low part from the sorted list
+
+// Step stream of a wide history (host-built, its own buffer):
+//   header word 0  live (bits 0..30), bit 31 clear
+//   header word 1  j (the returning slot), bit 31 clear
+//   op words, one per invocation since the previous step (<= DENSE_MAX_NINV), bit 31 set:
+//                  slot[0:8) | amask[8:16) | bmask[16:24) | DENSE_OPW
+//   a 0 word after the last step
+struct WideParams {
+  int32_t n;                  // wide histories in this launch (run one after another)
+  const int64_t* sbeg;        // [n] first word of each history's stream in `stream`
+  const int32_t* nsteps;      // [n]
+  const int8_t* lmax;         // [n] table width (slots)
+  const uint32_t* stream;
+  const uint32_t* words;      // the DENSE_WORD_BITS-bit sorted word list (dense_word_list)
+  uint64_t* tab;              // 2 tables of tab_words words each
+  int64_t tab_words;
+  int32_t* status;            // [n] ST_VALID / ST_INVALID
+  int32_t* fail_step;         // [n] the failing RETURN step (-1: none)
+  unsigned long long* explored;  // [n] (zeroed before launch)
+  unsigned long long* any;    // [n] latest step (+1) whose frontier held a config (zeroed)
+  unsigned* bar;              // grid barrier words (zeroed before launch)
+  int32_t* abort;             // a barrier watchdog fired
+  unsigned long long* stats;  // [2] frontier-out configs, steps
+};
+
+hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream);
+int wide_grid_size();
+size_t wide_bar_bytes();
+
+}  // namespace lc

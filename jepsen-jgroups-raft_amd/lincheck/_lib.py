@@ -21,7 +21,7 @@ EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_release", "lc_ch
            "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
            "lc_part_step_end", "lc_part_results", "lc_part_run", "lc_part_destroy", "lc_part_check")
 ABI_VERSION = 3
-STATS_N = 31
+STATS_N = 34
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
                "spill_inserts", "dense_histories", "dense_ms", "dense_big_ms", "dense_wave_ms",
@@ -29,7 +29,8 @@ STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candi
                "dense_wave_lds_bytes", "create_encode_ms", "create_device_init_ms",
                "create_streams_ms", "create_upload_ms", "create_dense_streams_ms",
                "dense_big_frontier_in", "dense_big_frontier_out", "dense_big_explored",
-               "dense_wave_frontier_in", "dense_wave_frontier_out", "dense_wave_explored")
+               "dense_wave_frontier_in", "dense_wave_frontier_out", "dense_wave_explored",
+               "wide_histories", "wide_ms", "wide_hbm_bytes")
 
 P = C.c_void_p
 I8P = C.POINTER(C.c_int8)

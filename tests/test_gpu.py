@@ -1029,3 +1029,91 @@ def test_gpu_bench_two_ranks_one_gpu(workload, tmp_path):
         assert out["configs_explored_per_s"] > 0
     else:
         assert out["verdict"]["bounds_ok"] is True
+
+
+# ---- closure tables in HBM (wide.hip): live width 25..30 -------------------
+
+@pytest.mark.parametrize("minw", ["1", "12"])
+def test_gpu_wide_tables_vs_oracle(minw, monkeypatch):
+    """The HBM-table kernel, with LC_WIDE_MINW routing every history from that width on to it
+    (in production it takes widths 25..30 only): random histories valid and invalid, 16-client
+    histories with crashed ops, the low-slot orderings and tiny/empty ones, one launch for all
+    of them, bit-exact with the oracle (verdict, failing op, its invocation, :previous-ok,
+    explored)."""
+    monkeypatch.setenv("LC_WIDE_MINW", minw)
+    rng = random.Random(5)
+    hs = [synth.gen_register(rng.randint(0, 60), rng.randint(1, 8), 0.2, 51000 + t, invalid=(t % 2 == 1))
+          for t in range(120)]
+    hs += [synth.gen_register(300, 16, 0.01, 52000 + t, invalid=(t % 2 == 1), n_crashed=2 + t) for t in range(4)]
+    hs += [_low_slot_rounds(30, 53000 + t, perturb=(t % 2 == 1)) for t in range(6)]
+    h = H.concat(hs)
+    widths = [_live_width(h, k) for k in range(h.n_hist)]
+    g = _lib.check(1, 0, h)
+    st = _lib.check_stats()
+    n_wide = sum(1 for w in widths if w >= int(minw))
+    assert st["wide_histories"] == n_wide and n_wide > 0, (st["wide_histories"], n_wide)
+    exp = oracle.check_many("cas-register", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"wide minw={minw} w={widths[k]}")
+    assert any(e["valid"] == 0 for e in exp) and max(widths) >= 17
+
+
+def test_gpu_wide_tables_match_tile_teams_at_width_24():
+    """At the tile teams' limit (width 24: 2.5-2.9 G configs explored) the HBM tables give the
+    tile team's explored count and verdict exactly (the crash-ramp histories K = 10, 12)."""
+    for k in (10, 12):
+        h = synth.gen_register(2000, 16, 0.002, 0x5EED4000 + k, n_crashed=k)
+        assert _live_width(h, 0) == 24
+        a = _lib.check(1, 0, h)
+        assert _lib.check_stats()["wide_histories"] == 0
+        os.environ["LC_WIDE_MINW"] = "24"
+        try:
+            b = _lib.check(1, 0, h)
+            assert _lib.check_stats()["wide_histories"] == 1
+        finally:
+            del os.environ["LC_WIDE_MINW"]
+        for key in ("valid", "fail_idx", "explored"):
+            assert int(a[key][0]) == int(b[key][0]), (k, key, a[key][0], b[key][0])
+        assert int(a["explored"][0]) > 2_000_000_000
+
+
+def _with_never_ops(h, n):
+    """h with n more calls pending for its whole length: cas 9 -> 8 by n extra processes,
+    invoked first and completed :info last. The register never holds 9, so no config ever
+    linearizes them: the verdict and the explored count are h's, the live width is h's + n."""
+    m = n + int(h.n) + n
+    proc = np.concatenate([10000 + np.arange(n), h.process, 10000 + np.arange(n)]).astype(np.int32)
+    typ = np.concatenate([np.zeros(n), h.type, np.full(n, 3)]).astype(np.int8)
+    f = np.concatenate([np.full(n, 2), h.f, np.full(n, 2)]).astype(np.int8)
+    v0 = np.concatenate([np.full(n, 9), h.v0, np.full(n, 9)]).astype(np.int64)
+    v1 = np.concatenate([np.full(n, 8), h.v1, np.full(n, 8)]).astype(np.int64)
+    vf = np.concatenate([np.full(n, H.V_PAIR), h.vflags, np.full(n, H.V_PAIR)]).astype(np.int8)
+    return H.from_columns(np.arange(m), proc, typ, f, v0, v1, vf)
+
+
+def test_gpu_wide_tables_past_the_tile_teams():
+    """Widths 25..30 against the oracle: 400-op histories of 14 clients plus up to 14 calls that
+    are pending throughout and can never apply (so the oracle's frontier stays small while the
+    tables are 2^22..2^27 words), valid and with a read of a value never written; then the crash
+    ramp's width-27 history (K = 13; the grid kernel did not finish it in 3 minutes)."""
+    for n, bad in ((11, False), (12, True), (14, False), (16, True)):
+        base = synth.gen_register(400, 14, 0.0, 54000 + n)
+        if bad:  # a read of a value the register never holds (7; the domain is 0..4)
+            reads = [i for i in range(base.n) if base.type[i] == 1 and base.f[i] == 0 and base.vflags[i] == H.V_SCALAR]
+            v0 = base.v0.copy()
+            v0[reads[len(reads) // 2]] = 7
+            base = H.from_columns(base.index, base.process, base.type, base.f, v0, base.v1, base.vflags)
+        h = _with_never_ops(base, n)
+        w = _live_width(h, 0)
+        assert 24 < w <= 30, w
+        g = _lib.check(1, 0, h)
+        assert _lib.check_stats()["wide_histories"] == 1
+        e = oracle.check_one("cas-register", h)
+        assert e["valid"] == (0 if bad else 1)
+        _cmp(g, e, 0, f"wide w={w}")
+        assert int(g["explored"][0]) == oracle.check_one("cas-register", base)["explored"]
+    h = synth.gen_register(2000, 16, 0.002, 0x5EED4000 + 13, n_crashed=13)
+    assert _live_width(h, 0) == 27
+    g = _lib.check(1, 0, h)
+    assert _lib.check_stats()["wide_histories"] == 1
+    assert int(g["valid"][0]) == 1 and int(g["explored"][0]) > 0

@@ -85,8 +85,13 @@ def gpu_leg(ops, clients, k, part, part_cap, q):
     out["lc_check"] = {"wall_s": time.perf_counter() - t, "valid": int(r["valid"][0]),
                        "explored": int(r["explored"][0]), "err": int(r["err"][0])}
     st = _lib.check_stats()
-    out["lc_check"]["path"] = "dense" if st.get("dense_histories", 0) > 0 else "grid"
+    out["lc_check"]["path"] = ("wide (HBM tables)" if st.get("wide_histories", 0) > 0
+                               else "dense" if st.get("dense_histories", 0) > 0 else "grid")
     out["lc_check"]["kernel_ms"] = st.get("kernel_ms")
+    if st.get("wide_histories", 0) > 0:  # HBM-table kernel: algorithmic bytes / its time vs 8 TB/s
+        out["lc_check"]["wide_ms"] = st["wide_ms"]
+        out["lc_check"]["wide_alg_gb"] = st["wide_hbm_bytes"] / 1e9
+        out["lc_check"]["wide_alg_gbps"] = st["wide_hbm_bytes"] / st["wide_ms"] / 1e6 if st["wide_ms"] else None
     if out["lc_check"]["wall_s"] < 30:  # a second (warm) run: the device's first-use cost is gone
         t = time.perf_counter()
         _lib.check(1, 0, h)
