@@ -363,6 +363,7 @@ struct lc_plan {
     if ((e = getenv("LC_PLAN_X")) && atof(e) > 0) plan_x = atof(e);
     if ((e = getenv("LC_PLAN_KB")) && atof(e) > 0) plan_kb = atof(e);
     if ((e = getenv("LC_PLAN_ROT"))) plan_rot = atoi(e) != 0;
+    if ((e = getenv("LC_PLAN_TM")) && atof(e) > 0) plan_tm = atof(e);
     if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
     if ((e = getenv("LC_TEAM_ROT_LB"))) rot_min_lb = atoi(e);
     if ((e = getenv("LC_TEAM_ROT_CHAIN"))) rot_chain_lb = atoi(e);
@@ -391,7 +392,7 @@ struct lc_plan {
     wide_maxw = WIDE_LMAX, wide_minw = 0;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 85967, pipe_env = false, plan_off = false;
-    plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
+    plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
     rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
     kfcap = klcap = 1 << 18;
     cell_cap = 256;
@@ -561,8 +562,9 @@ struct lc_plan {
     bool ok = !v.err && v.n_states <= DENSE_MAX_STATES;
     for (int64_t t = 0; t < v.n_steps && ok; ++t)  // a step's words must fit the decoders' window
       if (v.step_ninv[t] > DENSE_MAX_NINV) ok = false;
-    // wider than the LDS tile teams hold (or from LC_WIDE_MINW on, tests): tables in HBM
-    const int wmin = wide_minw > 0 ? wide_minw : dense_maxw + 1;
+    // wider than the LDS tile teams can hold (or from LC_WIDE_MINW on, tests): tables in HBM.
+    // (LC_DENSE_MAXW below 24 sends the widths between it and 25 to the grid kernel, as before.)
+    const int wmin = wide_minw > 0 ? wide_minw : DENSE_WIDE_LMAX + 1;
     if (ok && v.live_max >= wmin && v.live_max <= wide_maxw) {
       wide_sink(h, v);
       return false;  // (its invocation arrays stay: lc_failure_configs re-runs it on the grid kernel)
@@ -787,6 +789,9 @@ struct lc_plan {
   double plan_x = 1.57;  // LC_PLAN_X: the team model's cost per team bit (us per step)
   double plan_kb = 0.45;  // LC_PLAN_KB: the batch plan's VALU factor
   bool plan_rot = false;  // LC_PLAN_ROT: the team model knows which teams will be rotated
+  // LC_PLAN_TM: a batch plan's team estimates times this (r3n LC_DEBUG: rotated 17-slot teams
+  // took 1.3-1.8x their estimate while the BLOCK pool took 0.95x of its own)
+  double plan_tm = 1.0;
   // A batch plan (LC_BATCH_HIST: more than 600 histories, e.g. C3 on one GPU) fills the chip,
   // so the launch is throughput-bound; fewer histories leave workgroups idle and the launch is
   // its slowest chain (r2rot6-8: C3 1000 keys 11.8 ms batch / 16.2 unrotated; a 250-key share
@@ -819,7 +824,7 @@ struct lc_plan {
       else if (L > lb) u += 3.87 + plan_x * (L - lb);
       t += ws.c[L] * u;
     }
-    return t;
+    return batch_plan() ? t * plan_tm : t;
   }
   void plan_teams(const std::vector<WidthHist>& ws) {
     const bool pipe_teams = (dense_pipe & 12) == 12;
@@ -2269,6 +2274,16 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
     return LC_E_ARG;
   }
   const int t_fail = p->fail_step[0];
+  // a history wider than the LDS tables was decided on the HBM tables (wide.hip), which keep no
+  // per-config :last-op; its grid-kernel re-run can take minutes at these widths (the crash
+  // ramp's width-27 history did not finish in 3), so the report stops here unless asked
+  // (LC_WIDE_CONFIGS=1). The verdict, failing op and explored count stand.
+  if (p->enc.live_max[0] > DENSE_WIDE_LMAX && p->enc.model == LC_MODEL_CAS_REGISTER &&
+      !(getenv("LC_WIDE_CONFIGS") && atoi(getenv("LC_WIDE_CONFIGS")) != 0)) {
+    set_err(err, err_len, "failure configs unavailable: %d live slots (> %d: decided on the HBM tables)",
+            p->enc.live_max[0], DENSE_WIDE_LMAX);
+    return LC_E_CONFIGS;
+  }
   if (p->enc.live_max[0] + p->state_bits_of(0) + 6 > 63) {
     set_err(err, err_len, "failure configs unavailable: %d pending ops leave no room for the last-op tag",
             p->enc.live_max[0]);

@@ -1112,6 +1112,9 @@ def test_gpu_wide_tables_past_the_tile_teams():
         assert e["valid"] == (0 if bad else 1)
         _cmp(g, e, 0, f"wide w={w}")
         assert int(g["explored"][0]) == oracle.check_one("cas-register", base)["explored"]
+        if bad:  # no failure report from the HBM tables: LC_E_CONFIGS, the verdict stands
+            with pytest.raises(_lib.LincheckError, match="unavailable"):
+                _lib.failure_configs(0)
     h = synth.gen_register(2000, 16, 0.002, 0x5EED4000 + 13, n_crashed=13)
     assert _live_width(h, 0) == 27
     g = _lib.check(1, 0, h)
