@@ -14,6 +14,7 @@ timeout -k 10 300 $B --steps 20 --warmup 5 > $out/c3_bench.json 2> $out/c3_bench
 timeout -k 10 200 $B --workload c1 --steps 50 --warmup 10 > $out/c1_bench.json 2> $out/c1_bench.err || exit 1
 timeout -k 10 200 $B --workload c2 --steps 10 --warmup 2 > $out/c2_bench.json 2> $out/c2_bench.err || exit 1
 timeout -k 10 200 $B --workload c5 --steps 20 --warmup 5 > $out/c5_bench.json 2> $out/c5_bench.err || exit 1
+timeout -k 10 300 $B --workload c4 --steps 3 --warmup 1 > $out/c4_bench.json 2> $out/c4_bench.err || exit 1
 for r in 0 1 2 3 4 5 6 7; do
   timeout -k 10 120 $B --steps 10 --warmup 3 --no-cpu --e2e-reps 0 --emulate $r/8 > $out/c3_emulate_${r}of8.json 2> /dev/null || exit 1
 done
@@ -34,4 +35,8 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_
   --warmup 0 >> $out/pmc.log 2>&1 || exit 1
 # partitioned frontier: tools/profile_part.sh (its own call: rocprofv3 segfaults at exit after
 # tracing the cooperative part_step_kernel, once the trace is written)
+# the HBM-table kernel (crash ramp K = 16, width 30), last: it is a cooperative launch, and
+# rocprofv3 runs over cooperative kernels fault in the HIP runtime's exit handler after the
+# profile is written: one pass, the script's last GPU command, its exit status recorded
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/wide_trace -o run -- python -u tools/wide_once.py 16 > $out/wide_trace.log 2>&1; echo "wide trace exit $?" >> $out/pmc.log
 echo done
