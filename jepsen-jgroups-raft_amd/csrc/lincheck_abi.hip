@@ -169,6 +169,7 @@ struct lc_plan {
   std::vector<std::vector<uint32_t>> wide_streams;  // per history (built by dense_sink)
   DevArray d_wtab, d_wstream, d_wmeta, d_wres, d_wbar;
   int wide_maxw = WIDE_LMAX, wide_minw = 0;  // LC_WIDE_MAXW (0: off) / LC_WIDE_MINW (tests)
+  bool wide_pipe = true;  // LC_WIDE_PIPE=0: one step at a time (a grid barrier per popcount layer)
   // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
   // begin / step count / table width, and the queue order
   uint32_t* dp_stream = nullptr;
@@ -356,6 +357,7 @@ struct lc_plan {
     if ((e = getenv("LC_DENSE_MAXW")) && atoi(e) > 0) dense_maxw = std::min(atoi(e), DENSE_WIDE_LMAX);
     if ((e = getenv("LC_WIDE_MAXW"))) wide_maxw = std::max(0, std::min(atoi(e), WIDE_LMAX));
     if ((e = getenv("LC_WIDE_MINW"))) wide_minw = std::max(0, atoi(e));
+    if ((e = getenv("LC_WIDE_PIPE"))) wide_pipe = atoi(e) != 0;
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e), pipe_env = true;
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
@@ -389,7 +391,7 @@ struct lc_plan {
   void reset_knobs() {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
-    wide_maxw = WIDE_LMAX, wide_minw = 0;
+    wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 85967, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
@@ -1591,13 +1593,18 @@ struct lc_plan {
       dense_word_list(DENSE_WORD_BITS, wl.data());
       if ((rc = upload(d_dwords, wl))) return rc;
     }
-    // meta: sbeg | nsteps | lmax; results: explored | any | status | fail | stats[2]
+    // meta: sbeg | anyv_off | nsteps | lmax; results: explored | any | status | fail | stats[2] |
+    // the pipelined kernel's per-step bits
+    std::vector<int64_t> aoff(nwd);
+    int64_t abits = 0;
+    for (int i = 0; i < nwd; ++i) aoff[i] = abits, abits += nst[i] / 32 + 1;
     const size_t m_sb = (size_t)nwd * 8, m_ns = (size_t)nwd * 4;
-    HIP_TRY(d_wmeta.ensure(m_sb + m_ns + (size_t)nwd + 8));
+    HIP_TRY(d_wmeta.ensure(2 * m_sb + m_ns + (size_t)nwd + 8));
     HIP_TRY(hipMemcpy(d_wmeta.p, sbeg.data(), m_sb, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy((char*)d_wmeta.p + m_sb, nst.data(), m_ns, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy((char*)d_wmeta.p + m_sb + m_ns, lmx.data(), (size_t)nwd, hipMemcpyHostToDevice));
-    const size_t r_bytes = (size_t)nwd * 24 + 16;
+    HIP_TRY(hipMemcpy((char*)d_wmeta.p + m_sb, aoff.data(), m_sb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((char*)d_wmeta.p + 2 * m_sb, nst.data(), m_ns, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((char*)d_wmeta.p + 2 * m_sb + m_ns, lmx.data(), (size_t)nwd, hipMemcpyHostToDevice));
+    const size_t r_bytes = (size_t)nwd * 24 + 16 + (size_t)abits * 4;
     HIP_TRY(d_wres.ensure(r_bytes));
     HIP_TRY(d_wbar.ensure(wide_bar_bytes() + 8));
     HIP_TRY(hipMemsetAsync(d_wres.p, 0, r_bytes, stream));
@@ -1605,8 +1612,10 @@ struct lc_plan {
     WideParams p{};
     p.n = nwd;
     p.sbeg = (const int64_t*)d_wmeta.p;
-    p.nsteps = (const int32_t*)((char*)d_wmeta.p + m_sb);
-    p.lmax = (const int8_t*)((char*)d_wmeta.p + m_sb + m_ns);
+    p.anyv_off = (const int64_t*)((char*)d_wmeta.p + m_sb);
+    p.nsteps = (const int32_t*)((char*)d_wmeta.p + 2 * m_sb);
+    p.lmax = (const int8_t*)((char*)d_wmeta.p + 2 * m_sb + m_ns);
+    p.pipe = wide_pipe ? 1 : 0;
     p.stream = d_wstream.as<uint32_t>();
     p.words = d_dwords.as<uint32_t>();
     p.tab = d_wtab.as<uint64_t>();
@@ -1617,6 +1626,7 @@ struct lc_plan {
     p.status = (int32_t*)(rex + 2 * nwd);
     p.fail_step = p.status + nwd;
     p.stats = (unsigned long long*)(p.fail_step + nwd);
+    p.anyv = (uint32_t*)(p.stats + 2);
     p.bar = d_wbar.as<unsigned>();
     p.abort = (int32_t*)((char*)d_wbar.p + wide_bar_bytes());
     const int grid = wide_grid_size();

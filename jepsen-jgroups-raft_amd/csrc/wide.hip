@@ -266,6 +266,227 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
   if (blockIdx.x == 0 && tid == 0 && st_steps) atomicAdd(&p.stats[1], st_steps);
 }
 
+// ---- pipelined steps (WideParams.pipe): the schedule of dense.hip's history_pipe with the whole
+// grid as the team. Step t+1's layer q reads step t's words of popcount <= q + 1 (its X through
+// a hi return) or q (an in-word return) and writes words of popcount q on the other table, so it
+// runs in the same super-layer as step t's layer q + 2 (q + 1): a step starts two super-layers
+// after its predecessor (one after an in-word return; at once when the predecessor has retired)
+// and a grid barrier ends each super-layer, ~1.7 per step instead of H + 1. Step t shares its
+// table with step t - 2, which is at least two super-layers ahead (dense.hip §3.2's argument).
+// A super-layer's words are the running steps' layers, one flat index over the grid; a layer's
+// word g is (high part, low part) by popcount of the high part p (C(hb, p) highs of popcount p,
+// each with C(k, q - p) lows; both parts from the sorted word list), so no per-layer tables.
+// Failure: a workgroup that reads a nonzero X in step t sets bit t of `anyv`; when step t retires
+// (after its last layer's barrier) every workgroup reads the bit: 0 means step t - 1 returned an
+// empty frontier.
+constexpr int WRING = 16;
+struct WStep {
+  OpSel ops[32];
+  uint32_t live, fresh, foldm, j;
+  int32_t jp, H, start, pad;
+};
+
+__global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
+  __shared__ uint32_t sBin[WB * WB];
+  __shared__ uint32_t sLay[WIDE_LOW_BITS + 2];
+  __shared__ WStep sRing[WRING];
+  __shared__ uint32_t sSeg[WRING + 1];  // running segments' first flat index (+ the total)
+  __shared__ unsigned long long sRed;
+  __shared__ int sAbort;
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < WB * WB; i += WWG) {
+    const int n = i / WB, k = i % WB;
+    uint64_t c = 0;
+    if (k <= n) {
+      c = 1;
+      for (int q = 1; q <= k; ++q) c = c * (uint64_t)(n - k + q) / (uint64_t)q;
+    }
+    sBin[i] = (uint32_t)c;
+  }
+  if (tid == 0) sAbort = 0;
+  __syncthreads();
+  if (tid <= WIDE_LOW_BITS + 1) {
+    uint32_t o = 0;
+    for (int r = 0; r < tid; ++r) o += sBin[DENSE_WORD_BITS * WB + r];
+    sLay[tid] = o;
+  }
+  const int64_t gtid = (int64_t)blockIdx.x * WWG + tid, gstride = (int64_t)gridDim.x * WWG;
+  unsigned long long st_fout = 0, st_steps = 0;
+  for (int i = 0; i < p.n && !sAbort; ++i) {
+    const int ns = p.nsteps[i];
+    uint64_t* const T0 = p.tab;
+    uint64_t* const T1 = p.tab + p.tab_words;
+    auto tab = [&](int t) { return (t & 1) ? T1 : T0; };
+    uint32_t* const anyv = p.anyv + p.anyv_off[i];
+    if (blockIdx.x == 0 && tid == 0) HbmTab::st(&T1[0], 1ull);  // the initial config, read by step 0
+    int64_t pos = p.sbeg[i];
+    // decode step t into its ring slot (wave 0): the previous step's ops + this step's invocations
+    auto decode = [&](int t) {
+      if (tid >= 64) return;
+      WStep* dst = &sRing[t % WRING];
+      const WStep* prev = t > 0 ? &sRing[(t - 1) % WRING] : nullptr;
+      const uint32_t wd = p.stream[pos + lane];
+      const uint32_t live = (uint32_t)__shfl((int)wd, 0, 64), j = (uint32_t)__shfl((int)wd, 1, 64);
+      const unsigned long long ob = __ballot(lane >= 2 && lane < 2 + DENSE_MAX_NINV && (wd & DENSE_OPW));
+      const int ninv = (int)__builtin_ctzll(~(ob >> 2));
+      const uint32_t plive = prev ? prev->live : 0u;
+      const int pj = prev ? (int)prev->j : -1;
+      if (lane < 32) dst->ops[lane] = prev ? prev->ops[lane] : OpSel{SEL_NONE, SEL_NONE};
+      if (lane >= 2 && lane < 2 + ninv) dst->ops[wd & 31u] = decode_op((wd >> 8) & 0xffu, (wd >> 16) & 0xffu);
+      const uint32_t foldm = (uint32_t)__ballot(lane < 32 && dst->ops[lane & 31].hi == OPS_FOLD);
+      if (lane == 0) {
+        const int L = 32 - __clz((int)live);
+        dst->live = live;
+        dst->fresh = prev ? live & ~(plive & ~(1u << pj)) : live;
+        dst->foldm = foldm;
+        dst->j = j;
+        dst->jp = pj;
+        dst->H = L > 3 ? L - 3 : 0;
+        dst->start = 1 << 30;
+      }
+      pos += 2 + ninv;
+    };
+    if (ns > 0) decode(0);
+    __syncthreads();
+    if (ns > 0 && tid == 0) sRing[0].start = 0;
+    if (!wide_sync(p, &sAbort)) break;
+    unsigned long long expl = 0;
+    int fail_t = -1, t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0;
+    for (int s = 0; t_ret < ns; ++s) {
+      // ---- retire the steps whose last layer ran before this super-layer, in order
+      while (t_ret < t_run) {
+        const WStep& r = sRing[t_ret % WRING];
+        if (r.start + r.H >= s) break;
+        if (t_ret > 0 && !((ld_agent(&anyv[t_ret >> 5]) >> (t_ret & 31)) & 1u)) {  // same in every workgroup
+          fail_t = t_ret - 1;
+          break;
+        }
+        ++t_ret;
+        ++st_steps;
+      }
+      if (fail_t >= 0 || t_ret >= ns) break;
+      // ---- this super-layer's segments: running step t in its layer q = s - start (C(H, q) words)
+      if (tid <= WRING) {
+        uint32_t acc = 0;
+        for (int t = t_ret; t < t_run && t - t_ret < tid; ++t) {
+          const WStep& r = sRing[t % WRING];
+          const int q = s - r.start;
+          if (q >= 0 && q <= r.H) acc += sBin[r.H * WB + q];
+        }
+        sSeg[tid] = acc;
+      }
+      __syncthreads();
+      const uint32_t total = sSeg[t_run - t_ret];
+      uint32_t anyseg = 0;  // running steps (bit t - t_ret) in which this thread read a nonzero X
+      for (int64_t g = gtid; g < (int64_t)total; g += gstride) {
+        int si = 0;  // the segment holding g
+        while (si + 1 < t_run - t_ret && sSeg[si + 1] <= (uint32_t)g) ++si;
+        const int t = t_ret + si;
+        const WStep& r = sRing[t % WRING];
+        const int H = r.H, q = s - r.start;
+        const int k = H < WIDE_LOW_BITS ? H : WIDE_LOW_BITS, hb = H - k;
+        uint32_t gi = (uint32_t)g - sSeg[si];
+        int pp = q - k > 0 ? q - k : 0;  // the high part's popcount: blocks of C(hb, p) C(k, q - p)
+        for (;; ++pp) {
+          const uint32_t blk = sBin[hb * WB + pp] * sBin[k * WB + (q - pp)];
+          if (gi < blk || pp >= hb || pp >= q) break;
+          gi -= blk;
+        }
+        const uint32_t nlo = sBin[k * WB + (q - pp)];
+        const uint32_t hi_i = gi / nlo, lo_i = gi - hi_i * nlo;
+        const uint32_t w = (hb ? (p.words[sLay[pp] + hi_i] << k) : 0u) | p.words[sLay[q - pp] + lo_i];
+        const uint32_t live = r.live;
+        if (w & ~(live >> 3)) continue;
+        const uint32_t fresh = r.fresh, foldm = r.foldm;
+        const int j = (int)r.j, jp = r.jp;
+        uint64_t X = 0;
+        if (!(w & (fresh >> 3))) {
+          const uint64_t* Bp = tab(t - 1);
+          if (jp >= 3) X = HbmTab::ld(&Bp[w | (1u << (jp - 3))]);
+          else if (jp >= 0) X = (HbmTab::ld(&Bp[w]) & ~keep64(jp)) >> (1 << jp);
+          else X = HbmTab::ld(&Bp[w]);
+#pragma unroll
+          for (int kk = 0; kk < 3; ++kk)
+            if (fresh & (1u << kk)) X &= keep64(kk);
+        }
+        uint64_t* const B = tab(t);
+        uint64_t R = wide_pulls(B, w, j >= 3 ? 1u << (j - 3) : 0u, r.ops, foldm);
+        R = close_in_word(X, w, live, j, r.ops, foldm, R);
+        HbmTab::st(&B[w], X | R);
+        expl += (uint64_t)__popcll(R);
+        if (t > 0) st_fout += (uint64_t)__popcll(X);
+        if (X) anyseg |= 1u << si;
+      }
+      // the steps this wave saw a config in: one atomic OR per step per wave
+      for (int si = 0; si < t_run - t_ret; ++si)
+        if (__any((anyseg >> si) & 1u) && lane == 0) {
+          const int t = t_ret + si;
+          __hip_atomic_fetch_or(&anyv[t >> 5], 1u << (t & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      // ---- decode ahead into a free ring slot, and start the next step at s + 1: two
+      // super-layers after its predecessor (one after an in-word return, or the predecessor's
+      // H + 1 if fewer), at once if the predecessor has retired
+      const int t_dec_old = t_dec;
+      if (t_dec < ns && t_dec - t_ret < WRING - 1) {
+        decode(t_dec);
+        ++t_dec;
+      }
+      __syncthreads();
+      if (t_run < t_dec_old) {
+        bool ok = true;
+        if (t_run - 1 >= t_ret) {
+          const WStep& pr = sRing[(t_run - 1) % WRING];
+          const int gap = pr.j < 3 ? 1 : 2;
+          ok = s + 1 - pr.start >= min(gap, pr.H + 1);
+        }
+        if (ok) {
+          if (tid == 0) sRing[t_run % WRING].start = s + 1;
+          ++t_run;
+        }
+      }
+      if (!wide_sync(p, &sAbort)) break;
+    }
+    if (sAbort) break;
+    if (fail_t < 0 && ns > 0) {  // the last step's return: its frontier must hold a config
+      const WStep& r = sRing[(ns - 1) % WRING];
+      const int pj = (int)r.j;
+      const uint32_t lv = r.live & ~(1u << pj);
+      const int Lf = lv ? 32 - __clz((int)lv) : 0;
+      const int64_t nwt = (int64_t)1 << (Lf > 3 ? Lf - 3 : 0);
+      const uint64_t* const Bl = tab(ns - 1);
+      uint64_t nz = 0;
+      for (int64_t w = gtid; w < nwt; w += gstride) {
+        if ((uint32_t)w & ~(lv >> 3)) continue;
+        uint64_t X;
+        if (pj >= 3) X = HbmTab::ld(&Bl[(uint32_t)w | (1u << (pj - 3))]);
+        else X = (HbmTab::ld(&Bl[w]) & ~keep64(pj)) >> (1 << pj);
+        st_fout += (uint64_t)__popcll(X);
+        nz |= X;
+      }
+      if (__any(nz != 0) && lane == 0)
+        __hip_atomic_fetch_or(&anyv[ns >> 5], 1u << (ns & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!wide_sync(p, &sAbort)) break;
+      if (!((ld_agent(&anyv[ns >> 5]) >> (ns & 31)) & 1u)) fail_t = ns - 1;
+    }
+    for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
+    if (tid == 0) sRed = 0;
+    __syncthreads();
+    if (lane == 0 && expl) atomicAdd(&sRed, expl);
+    __syncthreads();
+    if (tid == 0) {
+      if (sRed) atomicAdd(&p.explored[i], sRed);
+      if (blockIdx.x == 0) {
+        p.status[i] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+        p.fail_step[i] = fail_t;
+      }
+    }
+    if (!wide_sync(p, &sAbort)) break;
+  }
+  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
+  if (lane == 0 && st_fout) atomicAdd(&p.stats[0], st_fout);
+  if (blockIdx.x == 0 && tid == 0 && st_steps) atomicAdd(&p.stats[1], st_steps);
+}
+
 }  // namespace
 
 int wide_grid_size() {
@@ -275,6 +496,9 @@ int wide_grid_size() {
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel, WWG, 0) != hipSuccess || per_cu < 1) return 0;
+  int per_cu2 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, wide_pipe_kernel, WWG, 0) != hipSuccess || per_cu2 < 1)
+    return 0;
   return prop.multiProcessorCount;  // one workgroup per CU: every workgroup resident
 }
 
@@ -283,7 +507,8 @@ size_t wide_bar_bytes() { return sizeof(WideBar); }
 hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream) {
   WideParams q = p;
   void* args[] = {&q};
-  return hipLaunchCooperativeKernel((const void*)wide_kernel, dim3(grid), dim3(WWG), args, 0, stream);
+  return hipLaunchCooperativeKernel(p.pipe ? (const void*)wide_pipe_kernel : (const void*)wide_kernel, dim3(grid),
+                                    dim3(WWG), args, 0, stream);
 }
 
 }  // namespace lc

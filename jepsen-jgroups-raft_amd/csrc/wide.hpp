@@ -39,6 +39,9 @@ struct WideParams {
   unsigned* bar;              // grid barrier words (zeroed before launch)
   int32_t* abort;             // a barrier watchdog fired
   unsigned long long* stats;  // [2] frontier-out configs, steps
+  int32_t pipe;               // 1: pipelined steps (wide_pipe_kernel), 0: one step at a time
+  uint32_t* anyv;             // pipelined: per history, bit t = some X of step t was nonzero (zeroed)
+  const int64_t* anyv_off;    // [n] word offset of each history's bits (ns / 32 + 1 words)
 };
 
 hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream);
