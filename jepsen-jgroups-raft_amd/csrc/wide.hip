@@ -11,8 +11,8 @@
 //                  grid barrier
 // so the DP is dense.hip's run_layers with the layers as grid-wide phases. A layer's words are
 // (high part a, low part from the sorted word list): w = a << k | low, k = min(H, 19), the
-// 2^(H-k) <= 256 high parts in a per-layer prefix table (LDS), so a thread's word comes from a
-// binary search over <= 8 entries and one list load, and consecutive threads take consecutive
+// 2^(H-k) <= 512 high parts in a per-layer prefix table (LDS), so a thread's word comes from a
+// binary search over <= 9 entries and one list load, and consecutive threads take consecutive
 // low words of one high part (neighbouring table words).
 // Failure: each step ORs "some X was nonzero" (step t-1's post-return frontier held a config)
 // into `any` as an atomicMax of t + 1 before its last barrier; after it every workgroup reads
@@ -29,7 +29,7 @@ namespace {
 constexpr int WWG = 1024;
 constexpr int WB = 32;  // binomials C(n, k) for n < 32 (u32: C(31, 15) = 300,540,195)
 constexpr int WH = WIDE_LMAX - 3;  // most hi bits
-constexpr int WPRE = 257;          // per layer: prefix over <= 256 high parts, + the total
+constexpr int WPRE = 513;          // per layer: prefix over <= 512 high parts, + the total
 
 struct WideBar {  // two-level arrival counters + generation, each on its own 128-B lines
   unsigned grp[8][32];

@@ -14,7 +14,7 @@
 
 namespace lc {
 
-constexpr int WIDE_LMAX = 30;       // widest history: 2 tables of 2^27 words (2 GiB)
+constexpr int WIDE_LMAX = 31;       // widest history: 2 tables of 2^28 words (4 GiB); slots <= 30 keep bit 31 of a stream header clear
 constexpr int WIDE_LOW_BITS = 19;   // a layer's words = high part x low part from the sorted list
 
 // Step stream of a wide history (host-built, its own buffer):

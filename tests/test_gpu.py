@@ -1031,13 +1031,13 @@ def test_gpu_bench_two_ranks_one_gpu(workload, tmp_path):
         assert out["verdict"]["bounds_ok"] is True
 
 
-# ---- closure tables in HBM (wide.hip): live width 25..30 -------------------
+# ---- closure tables in HBM (wide.hip): live width 25..31 -------------------
 
 @pytest.mark.parametrize("pipe", ["1", "0"])
 @pytest.mark.parametrize("minw", ["1", "12"])
 def test_gpu_wide_tables_vs_oracle(minw, pipe, monkeypatch):
     """The HBM-table kernel, with LC_WIDE_MINW routing every history from that width on to it
-    (in production it takes widths 25..30 only): random histories valid and invalid, 16-client
+    (in production it takes widths 25..31 only): random histories valid and invalid, 16-client
     histories with crashed ops, the low-slot orderings and tiny/empty ones, one launch for all
     of them, bit-exact with the oracle (verdict, failing op, its invocation, :previous-ok,
     explored). LC_WIDE_PIPE=1 (the default) overlaps consecutive steps on the grid, 0 runs one
@@ -1095,12 +1095,13 @@ def _with_never_ops(h, n):
 
 
 def test_gpu_wide_tables_past_the_tile_teams():
-    """Widths 25..30 against the oracle: 400-op histories of 14 clients plus up to 14 calls that
+    """Widths 25..31 against the oracle: 400-op histories of 14 clients plus up to 18 calls that
     are pending throughout and can never apply (so the oracle's frontier stays small while the
     tables are 2^22..2^27 words), valid and with a read of a value never written; then the crash
     ramp's width-27 history (K = 13; the grid kernel did not finish it in 3 minutes)."""
-    for n, bad in ((11, False), (12, True), (14, False), (16, True)):
-        base = synth.gen_register(400, 14, 0.0, 54000 + n)
+    for n, bad, seed in ((11, False, 54011), (12, True, 54012), (14, False, 54014), (16, True, 54016),
+                         (18, False, 54000)):  # (the last one: width 31, the limit)
+        base = synth.gen_register(400, 14, 0.0, seed)
         if bad:  # a read of a value the register never holds (7; the domain is 0..4)
             reads = [i for i in range(base.n) if base.type[i] == 1 and base.f[i] == 0 and base.vflags[i] == H.V_SCALAR]
             v0 = base.v0.copy()
@@ -1108,7 +1109,7 @@ def test_gpu_wide_tables_past_the_tile_teams():
             base = H.from_columns(base.index, base.process, base.type, base.f, v0, base.v1, base.vflags)
         h = _with_never_ops(base, n)
         w = _live_width(h, 0)
-        assert 24 < w <= 30, w
+        assert 24 < w <= 31, w
         g = _lib.check(1, 0, h)
         assert _lib.check_stats()["wide_histories"] == 1
         e = oracle.check_one("cas-register", h)
