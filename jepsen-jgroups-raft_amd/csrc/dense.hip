@@ -1244,6 +1244,7 @@ constexpr int PIPE_XCD = 16384;  // XCD-compact workgroup roles in the big kerne
 // tile teams: credit tokens pre-polled a super-layer early (r3n A/B, 2 runs each: C2 30.08 ->
 // 29.92 ms, 8-way shares 0/1 7.14 -> 7.12 / 7.03 -> 6.97, C3 11.46 -> 11.44)
 constexpr int PIPE_CPRE = 65536;
+constexpr int PIPE_CW16 = 131072;  // tile teams: a credit window of 16 super-layers (default 8)
 
 __device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
                                            unsigned long long need, uint64_t t0, long& spins) {
@@ -1323,10 +1324,14 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   // check (lane = tile, 64 tiles per register), so the check's first poll costs no HBM round
   // trip when nobody lags (tokens only grow: an early value that suffices stays valid)
   unsigned long long cpre[4] = {0, 0, 0, 0};
+  // the credit window (super-layers a tile may run ahead of the slowest): 8, or 16 with
+  // PIPE_CW16 (a mirror slot is a step's, reused 64 steps later: >= 64 super-layers, more than
+  // the window's lag of 2 x 16 plus a step's span of at most H + T + 1 <= 25)
+  const int cw = (p.pipe & PIPE_CW16) ? 16 : 8;
   static_assert((1 << DENSE_TEAM_MAXB) <= 4 * 64, "credit pre-poll registers");
   for (int s = 0; t_ret < ns; ++s) {
     unsigned long long tp = timed ? now() : 0;
-    if (s >= 8 && (s & 7) == 0) {  // credit: nobody more than 8 super-layers behind
+    if (s >= cw && (s & (cw - 1)) == 0) {  // credit: nobody more than cw super-layers behind
       if (decoder) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         long spins = 0;
@@ -1334,8 +1339,8 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         for (int k = 0; k < 4; ++k) {  // one lane per tile, 64 tiles at a time
           const int r = 64 * k + lane;
           if (64 * k >= G) break;
-          const bool pre_ok = r >= G || cpre[k] >= (unsigned long long)(s - 8);
-          while (!__all(pre_ok || poll_until(p, &flags[r < G ? r : 0], (unsigned long long)(s - 8), t0, spins)))
+          const bool pre_ok = r >= G || cpre[k] >= (unsigned long long)(s - cw);
+          while (!__all(pre_ok || poll_until(p, &flags[r < G ? r : 0], (unsigned long long)(s - cw), t0, spins)))
             ;
         }
         if (lane == 0) *sAbort = ld_agent(p.abort);
@@ -1344,7 +1349,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
       if (*sAbort) break;
       if (timed) ph[3] += now() - tp, tp = now();
     }
-    if (decoder && (p.pipe & PIPE_CPRE) && s >= 7 && (s & 7) == 7) {  // the next check's tokens, loaded now
+    if (decoder && (p.pipe & PIPE_CPRE) && s >= cw - 1 && (s & (cw - 1)) == cw - 1) {  // the next check's tokens, loaded now
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         cpre[k] = 64 * k + lane < G ? ld_agent(&flags[64 * k + lane]) : 0ull;

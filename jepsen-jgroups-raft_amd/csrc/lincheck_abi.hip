@@ -1908,8 +1908,11 @@ void lpt_shards(int n_hist, const int64_t* off, int G, int32_t* out_shard) {
 // would run in a shard of a few hundred keys (a chain plan): WAVE (width <= 11) 7.9 us per
 // step, MID (12..14) 4.9 + 0.0016 * 2^(L-3), BLOCK (15..17) 4.67 + 0.00266 * 2^(L-3), wider a
 // tile team of 16-slot tiles, 1.59 + 0.0043 * 2^(min(L,16)-3) + [L > 16] (3.87 + 1.57 (L-16)).
-// Counter histories and histories the dense tables do not take (the grid kernel) cost their
-// entry count (one unit per entry). Host only.
+// Width 25..WIDE_LMAX (the HBM tables, a whole GPU each, one after another): per step ~7 us of
+// grid barriers plus its 2^n live words' X, pulls and store (8 B each) at ~1.3 TB/s (r3t/r3u:
+// 55 us per step at width 27, 190 at width 30 on the crash ramp). Counter histories and
+// histories no table takes (the grid kernel) cost their entry count (one unit per entry). Host
+// only.
 void history_costs(int model, int64_t init_value, int n_hist, const int64_t* off, const HistArrays& a,
                    std::vector<double>& cost) {
   cost.assign(n_hist, 0.0);
@@ -1921,12 +1924,22 @@ void history_costs(int model, int64_t init_value, int n_hist, const int64_t* off
   encode(model, init_value, n_hist, off, a, enc);
   for (int h = 0; h < n_hist; ++h) {
     const int lw = enc.live_max[h];
-    if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || lw > DENSE_WIDE_LMAX) {
+    if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || lw > WIDE_LMAX) {
       cost[h] = (double)(off[h + 1] - off[h]);
       continue;
     }
     uint64_t live = 0;
     double t = 0;
+    if (lw > DENSE_WIDE_LMAX) {  // the HBM tables
+      for (int64_t g = enc.step_off[h]; g < enc.step_off[h + 1]; ++g) {
+        if (g > enc.step_off[h]) live &= ~(1ull << enc.step_slot[g - 1]);
+        for (int64_t q = enc.inv_off[g]; q < enc.inv_off[g + 1]; ++q) live |= 1ull << enc.inv_slot[q];
+        const int n = __builtin_popcountll(live >> 3);
+        t += 7.0 + std::ldexp(1.0, n) * (n / 2.0 + 2.0) * 8.0 / 1.3e6;
+      }
+      cost[h] = t;
+      continue;
+    }
     for (int64_t g = enc.step_off[h]; g < enc.step_off[h + 1]; ++g) {
       if (g > enc.step_off[h]) live &= ~(1ull << enc.step_slot[g - 1]);
       for (int64_t q = enc.inv_off[g]; q < enc.inv_off[g + 1]; ++q) live |= 1ull << enc.inv_slot[q];
