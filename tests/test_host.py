@@ -302,6 +302,22 @@ def test_shard_histories_by_cost(n_shards):
     assert list(ccost) == [float(c.off[k + 1] - c.off[k]) for k in range(3)]
 
 
+def test_shard_cost_of_hbm_table_histories():
+    """Histories of width 25..31 (the HBM tables) are priced per step as ~7 us of
+    grid barriers plus their live words' bytes at 1.3 TB/s, not by entry count: the crash ramp's
+    width-27/30 histories (K = 13, 16) cost tens to hundreds of ms, far above a C3 key, and LPT
+    gives each its own shard."""
+    hs = [synth.gen_register(2000, 16, 0.002, 0x5EED4000 + k, n_crashed=k) for k in (13, 16)]
+    hs += [synth.gen_register(1000, 5, 0.01, 70 + k) for k in range(6)]
+    h = H.concat(hs)
+    shard, cost = _lib.shard_histories_by_cost(1, 0, h, 3)
+    steps = [int(np.sum((h.sub(k).type == 1))) for k in range(2)]
+    for k in range(2):
+        assert cost[k] >= 7.0 * steps[k] * 0.5 and cost[k] > 5 * cost[2:].max(), (k, cost[k])
+    assert 20_000 < cost[0] < 200_000 and 100_000 < cost[1] < 1_000_000  # us (measured 81 / 278 ms)
+    assert shard[0] != shard[1] and not set(shard[2:]) & {shard[1]}
+
+
 def test_shard_histories_rejects_bad_args():
     L = _lib.load()
     off = np.array([0, 5, 3], np.int64)  # not monotone
