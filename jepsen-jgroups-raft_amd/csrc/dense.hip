@@ -1244,7 +1244,7 @@ constexpr int PIPE_XCD = 16384;  // XCD-compact workgroup roles in the big kerne
 // tile teams: credit tokens pre-polled a super-layer early (r3n A/B, 2 runs each: C2 30.08 ->
 // 29.92 ms, 8-way shares 0/1 7.14 -> 7.12 / 7.03 -> 6.97, C3 11.46 -> 11.44)
 constexpr int PIPE_CPRE = 65536;
-constexpr int PIPE_CW16 = 131072;  // tile teams: a credit window of 16 super-layers (default 8)
+constexpr int PIPE_CW16 = 131072;  // tile teams: a credit window of 16 super-layers (else 8)
 
 __device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
                                            unsigned long long need, uint64_t t0, long& spins) {

@@ -217,9 +217,11 @@ struct lc_plan {
   // -> 11.59 ms); bit 12 = X of a step after a hi return from its inputs (off); bit 13 = tile
   // teams on global popcount layers (off); bit 14 = XCD-compact workgroup roles in the big
   // kernel (r3l A/B, 2 runs each: C3 11.64 -> 11.55 ms, C2 and 8-way shares unchanged); bit 16 =
-  // tile teams pre-poll their credit tokens a super-layer early (r3n: -0.5 to -1 %).
-  // Default 85967 = 1|2|4|8|64|128|256|512|1024|2048|16384|65536, with the planner.
-  int dense_pipe = 85967;
+  // tile teams pre-poll their credit tokens a super-layer early (r3n: -0.5 to -1 %); bit 17 = a
+  // credit window of 16 super-layers instead of 8 (r3y, 2 runs each: C2 30.09 -> 29.76, C3 11.52
+  // -> 11.39, C4 736 -> 729 ms, 8-way shares 0/1 unchanged).
+  // Default 217039 = 1|2|4|8|64|128|256|512|1024|2048|16384|65536|131072, with the planner.
+  int dense_pipe = 217039;
   bool pipe_env = false;  // LC_PIPE given: its bits as they are
   std::vector<int> plan_lb;  // team planner: local slots per tile (0: not a team)
   bool plan_off = false;     // LC_TEAM_PLAN=0: every wide history keeps 17-bit tiles
@@ -393,7 +395,7 @@ struct lc_plan {
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true;
     wide_from = 99, wide_lbits = DENSE_LMAX;
-    dense_pipe = 85967, pipe_env = false, plan_off = false;
+    dense_pipe = 217039, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
     rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
     kfcap = klcap = 1 << 18;

@@ -534,7 +534,7 @@ def test_gpu_dense_team_planner(plan, monkeypatch):
 
 @pytest.mark.parametrize("pipe", ["0", "1", "2", "3", "11", "15", "27", "47", "79", "143", "207",
                                   "515", "539", "591", "719", "975", "1999", "3139", "4047", "8143",
-                                  "12239", "20431", "28623", "85967"])
+                                  "12239", "20431", "28623", "85967", "217039"])
 def test_gpu_dense_pipelined_steps(pipe, monkeypatch):
     """LC_PIPE bit 0 / bit 1: BLOCK / WAVE teams overlap consecutive RETURN steps (step t+1's
     layer q beside step t's layer q + 2, returns read through the previous step's slot, fresh
