@@ -1245,7 +1245,6 @@ constexpr int PIPE_XCD = 16384;  // XCD-compact workgroup roles in the big kerne
 // 29.92 ms, 8-way shares 0/1 7.14 -> 7.12 / 7.03 -> 6.97, C3 11.46 -> 11.44)
 constexpr int PIPE_CPRE = 65536;
 constexpr int PIPE_CW16 = 131072;  // tile teams: a credit window of 16 super-layers (else 8)
-constexpr int PIPE_XPRE = 262144;  // tagged tile teams: X words of team-slot returns staged a super-layer early
 
 __device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
                                            unsigned long long need, uint64_t t0, long& spins) {
@@ -1276,11 +1275,9 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   // histories do: a word's index is then an LDS read, not a global load, on every word's chain
   const uint32_t* words = p.words;
   const uint32_t* wof = wofs;
-  size_t lds_used = (size_t)(dbl ? 2 : 1) << (lb - 3);  // u64 words of the LDS table in use
   {
     const int Hm = lb - 3, ntab = (dbl ? 2 : 1) << Hm;
     if (Hm >= 1 && ntab + (1 << Hm) / 2 + 16 <= (1 << HSOLO)) {
-      lds_used = (size_t)ntab + (1 << Hm) / 2 + 16;
       uint32_t* lw = reinterpret_cast<uint32_t*>(B + ntab);
       uint32_t* lo = lw + (1 << Hm);
       if (tid <= Hm + 1) {
@@ -1308,21 +1305,6 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
     return p.mirror + (((size_t)(base + r) * MRING + (size_t)(t % MRING)) << mshift);
   };
   auto tag_of = [&](int t) { return p.mirror_tag + (uint32_t)t + 1u; };
-  // X prefetch (LC_PIPE bit 18, tagged teams): a step after a team-slot return reads its X from
-  // tile xs = r | jp, words the previous step wrote at least two super-layers back. At the end
-  // of super-layer s (after this tile's own words, while it would wait at the barrier for its
-  // slowest wave anyway) every thread loads, once and without polling, the X words of the layer
-  // each such step runs at s + 1 into an LDS staging slot beside the tables; in s + 1 a word
-  // takes its X from there when the slot holds that (step, layer) and its granule tags matched,
-  // else it polls the mirror as before. Slots: [s + 1 parity][step mod XP_SLOTS], XP_WORDS words
-  // + a validity bit each; layers wider than a slot are not staged.
-  constexpr int XP_SLOTS = 4, XP_WORDS = 512;
-  constexpr size_t XP_U64 = 2 * XP_SLOTS * XP_WORDS + 2 * XP_SLOTS * (XP_WORDS / 64) + 2 * XP_SLOTS;
-  uint64_t* const xp_data = ((p.pipe & PIPE_XPRE) && tagged && lds_used + XP_U64 <= ((size_t)1 << HSOLO))
-                                ? B + lds_used : nullptr;
-  uint64_t* const xp_mask = xp_data ? xp_data + 2 * XP_SLOTS * XP_WORDS : nullptr;
-  int2* const xp_desc = xp_data ? reinterpret_cast<int2*>(xp_mask + 2 * XP_SLOTS * (XP_WORDS / 64)) : nullptr;
-  if (xp_desc && tid < 2 * XP_SLOTS) xp_desc[tid] = make_int2(-1, -1);  // (ordered by the barriers below)
   const int ns = p.nsteps[h];
   // LC_DEBUG phase cycles: pred/X waits, segments, publish + token, credit waits, -, super-layers
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
@@ -1487,15 +1469,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         // expanded); a tile holding j takes only T_j of r \ j
         const bool pl = tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u));
         if (tagged) {
-          if (fx && xs >= 0) {
-            const int xsl = (s & 1) * XP_SLOTS + t % XP_SLOTS;
-            const int2 d = xp_desc ? xp_desc[xsl] : make_int2(-1, -1);
-            if (d.x == t && d.y == rdl(q_l, i) && r < (uint32_t)XP_WORDS &&
-                ((xp_mask[xsl * (XP_WORDS / 64) + (r >> 6)] >> (r & 63)) & 1ull))
-              xv = xp_data[(size_t)xsl * XP_WORDS + r];
-            else
-              xv = TagTab::ld(mirror(xs, t - 1), mp + r, tag_of(t - 1), p.abort);
-          }
+          if (fx && xs >= 0) xv = TagTab::ld(mirror(xs, t - 1), mp + r, tag_of(t - 1), p.abort);
 #pragma unroll
           for (int b = 0; b < TB; ++b)
             pv[b] = (pl && ((pmask >> b) & 1u)) ? TagTab::ld(mirror(rank ^ (1 << b), t), mo + r, tag_of(t), p.abort)
@@ -1631,43 +1605,6 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
       i = i2;
 #pragma unroll
       for (int k = 0; k < TW; ++k) wn[k] = wn2[k];
-    }
-    if (xp_data) {  // stage the X words of the steps that run their next layer at s + 1 from tile xs
-      const int par = (s + 1) & 1;
-      uint64_t cand = __ballot(seg_l && xs_l >= 0 && q_l + 1 <= h1.z && !((uint32_t)rank & (h0.y >> lb)));
-      for (; cand; cand &= cand - 1) {
-        const int i = (int)__builtin_ctzll(cand);
-        const int t = t_ret_old + i;
-        const int H = rdl(h1.z, i), q1 = rdl(q_l, i) + 1, hp = rdl(h2.y, i), xs = rdl(xs_l, i);
-        const uint32_t nq1 = binom[H * BINOM_N + q1];
-        const int xsl = par * XP_SLOTS + t % XP_SLOTS;
-        if (nq1 > (uint32_t)XP_WORDS) {
-          if (tid == 0) xp_desc[xsl] = make_int2(-1, -1);
-          continue;
-        }
-        const uint32_t o1 = wof[q1], mp1 = cum[hp * BINOM_N + min(q1, hp)];
-        const uint32_t live_hi = (rdl(h0.x, i) & lmask) >> 3, fresh_hi = (rdl(h0.y, i) & lmask) >> 3;
-        const uint64_t* const src = mirror(xs, t - 1);
-        const uint32_t tg = tag_of(t - 1);
-        for (uint32_t r0 = (uint32_t)(tid & ~63); r0 < nq1; r0 += 1024u) {
-          const uint32_t r = r0 + (uint32_t)lane;
-          bool ok = false;
-          uint64_t v = 0;
-          if (r < nq1) {
-            const uint32_t w = words[o1 + r];
-            if (!(w & ~live_hi) && !(w & fresh_hi)) {  // a word the consumer reads X for
-              const uint64_t a = HbmTab::ld(&src[2 * (size_t)(mp1 + r)]);
-              const uint64_t b = HbmTab::ld(&src[2 * (size_t)(mp1 + r) + 1]);
-              ok = (uint32_t)(a >> 32) == tg && (uint32_t)(b >> 32) == tg;  // one try, no polling
-              v = (uint32_t)a | (b << 32);
-            }
-          }
-          const uint64_t m = __ballot(ok);
-          if (r < (uint32_t)XP_WORDS) xp_data[(size_t)xsl * XP_WORDS + r] = v;
-          if (lane == 0) xp_mask[xsl * (XP_WORDS / 64) + (r0 >> 6)] = m;
-        }
-        if (tid == 0) xp_desc[xsl] = make_int2(t, q1);
-      }
     }
     const int t_dec_old = t_dec;
     if (t_dec < ns && t_dec - t_ret_old < RING) {
