@@ -1245,6 +1245,7 @@ constexpr int PIPE_XCD = 16384;  // XCD-compact workgroup roles in the big kerne
 // 29.92 ms, 8-way shares 0/1 7.14 -> 7.12 / 7.03 -> 6.97, C3 11.46 -> 11.44)
 constexpr int PIPE_CPRE = 65536;
 constexpr int PIPE_CW16 = 131072;  // tile teams: a credit window of 16 super-layers (else 8)
+constexpr int PIPE_WSPREAD = 262144;  // big kernel: WAVE histories one per workgroup (big_wave_mode)
 
 __device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
                                            unsigned long long need, uint64_t t0, long& spins) {
@@ -1695,6 +1696,10 @@ __device__ __forceinline__ void big_wave_mode(const DenseParams& p, uint64_t* sT
   DenseParams q = p;
   q.n = p.n_w, q.order = p.order_w, q.queue = p.queue_w;
   const int w = tid / 64;
+  // LC_PIPE bit 18 (PIPE_WSPREAD, a plan of few WAVE histories): one wave per workgroup dequeues,
+  // so each history's wave has a CU to itself (a REG history's step is VALU/shuffle work that
+  // 16 waves on one CU would share)
+  if (!(p.pipe & PIPE_WSPREAD) || w == 0)
   history_pipe<64, DENSE_WAVE_LMAX, WAVE_RING, false, SLW>(q, tabs + w * SLW, zero, rings + w * WAVE_RING, &sQw[w],
                                                           &sEx[w], words, wofs, binom, tid & 63, st_fout, st_steps);
   __syncthreads();
@@ -1796,7 +1801,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   if (bid >= p.n_team_wgs) {  // ------------------------------------------------ BLOCK histories
     // the last ceil(n_w / 16) workgroups start on the WAVE queue: a WAVE history is a long
     // latency-bound chain, and started after the BLOCK queue it would be the launch's tail
-    const int wave_first = p.n_w > 0 ? (p.n_w + 15) / 16 : 0;
+    const int wave_first = p.n_w > 0 ? ((p.pipe & PIPE_WSPREAD) ? min(p.n_w, (int)gridDim.x - p.n_team_wgs) : (p.n_w + 15) / 16) : 0;
     if (wave_first && bid >= (int)gridDim.x - wave_first)
       big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     // and the next mid_first start on the MID queue (long chains too, four per workgroup)

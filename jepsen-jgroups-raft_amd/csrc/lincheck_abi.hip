@@ -1111,11 +1111,13 @@ struct lc_plan {
           q.tstamps = d_tstamps.as<unsigned long long>();
         }
       }
-      const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n + q.n2 + (q.n_w + 15) / 16));
+      // WAVE histories: 16 per workgroup, or one per workgroup under LC_PIPE bit 18 (PIPE_WSPREAD)
+      const int wave_wgs = (q.pipe & 262144) ? q.n_w : (q.n_w + 15) / 16;
+      const int grid = twgs + std::max(0, std::min(dgrid_b - twgs, q.n + q.n2 + wave_wgs));
       // BLOCK-pool workgroups that start on the MID queue: its share of the pool's work
       q.mid_first = 0;
       if (mid_in_big && q.n2 > 0) {
-        const int pool_wgs = grid - twgs - (q.n_w + 15) / 16;
+        const int pool_wgs = grid - twgs - wave_wgs;
         const double tot = pool_block_us + pool_mid_us + pool_wave_us;
         const double share = tot > 0 ? pool_mid_us / tot : 0.0;
         q.mid_first = std::max(0, std::min({(q.n2 + 3) / 4, pool_wgs, (int)std::lround(share * (grid - twgs))}));
