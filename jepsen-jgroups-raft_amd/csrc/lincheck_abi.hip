@@ -169,6 +169,7 @@ struct lc_plan {
   std::vector<std::vector<uint32_t>> wide_streams;  // per history (built by dense_sink)
   DevArray d_wtab, d_wstream, d_wmeta, d_wres, d_wbar;
   int wide_maxw = WIDE_LMAX, wide_minw = 0;  // LC_WIDE_MAXW (0: off) / LC_WIDE_MINW (tests)
+  int wide_grid = 0;  // LC_WIDE_GRID: at most this many workgroups for the HBM tables (0: one per CU)
   bool wide_pipe = true;  // LC_WIDE_PIPE=0: one step at a time (a grid barrier per popcount layer)
   // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
   // begin / step count / table width, and the queue order
@@ -360,6 +361,7 @@ struct lc_plan {
     if ((e = getenv("LC_WIDE_MAXW"))) wide_maxw = std::max(0, std::min(atoi(e), WIDE_LMAX));
     if ((e = getenv("LC_WIDE_MINW"))) wide_minw = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_PIPE"))) wide_pipe = atoi(e) != 0;
+    if ((e = getenv("LC_WIDE_GRID"))) wide_grid = std::max(0, atoi(e));
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e), pipe_env = true;
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
@@ -393,7 +395,7 @@ struct lc_plan {
   void reset_knobs() {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
-    wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true;
+    wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
@@ -1633,7 +1635,7 @@ struct lc_plan {
     p.anyv = (uint32_t*)(p.stats + 2);
     p.bar = d_wbar.as<unsigned>();
     p.abort = (int32_t*)((char*)d_wbar.p + wide_bar_bytes());
-    const int grid = wide_grid_size();
+    const int grid = wide_grid > 0 ? std::min(wide_grid, wide_grid_size()) : wide_grid_size();
     if (grid < 1) {
       last_error = "wide kernel: no resident workgroups";
       return LC_E_INTERNAL;
