@@ -370,6 +370,7 @@ struct lc_plan {
     if ((e = getenv("LC_PLAN_KB")) && atof(e) > 0) plan_kb = atof(e);
     if ((e = getenv("LC_PLAN_ROT"))) plan_rot = atoi(e) != 0;
     if ((e = getenv("LC_PLAN_TM")) && atof(e) > 0) plan_tm = atof(e);
+    if ((e = getenv("LC_PLAN_LBMIN")) && atoi(e) >= 4) plan_lbmin = atoi(e);
     if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
     if ((e = getenv("LC_TEAM_ROT_LB"))) rot_min_lb = atoi(e);
     if ((e = getenv("LC_TEAM_ROT_CHAIN"))) rot_chain_lb = atoi(e);
@@ -398,7 +399,7 @@ struct lc_plan {
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
-    plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
+    plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 13, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
     rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
     kfcap = klcap = 1 << 18;
     cell_cap = 256;
@@ -798,6 +799,7 @@ struct lc_plan {
   // LC_PLAN_TM: a batch plan's team estimates times this (r3n LC_DEBUG: rotated 17-slot teams
   // took 1.3-1.8x their estimate while the BLOCK pool took 0.95x of its own)
   double plan_tm = 1.0;
+  int plan_lbmin = 13;  // LC_PLAN_LBMIN: the team planner's smallest tile (local slots)
   // A batch plan (LC_BATCH_HIST: more than 600 histories, e.g. C3 on one GPU) fills the chip,
   // so the launch is throughput-bound; fewer histories leave workgroups idle and the launch is
   // its slowest chain (r2rot6-8: C3 1000 keys 11.8 ms batch / 16.2 unrotated; a 250-key share
@@ -864,7 +866,7 @@ struct lc_plan {
       // every smaller tile size the team limits allow: the one with the smallest makespan
       int nlb = -1, extra = 0;
       double t_new = est[best], m_best = est[best];
-      for (int lb = cur - 1; lb >= 13 && lw - lb <= maxb; --lb) {
+      for (int lb = cur - 1; lb >= plan_lbmin && lw - lb <= maxb; --lb) {
         const int x = wgs(best, lb) - (in_block[best] ? 1 : wgs(best, cur));
         if (team_wgs + x > cap || dgrid_b - team_wgs - x < 1) break;
         const double t = est_team_us(ws[best], lb, lw);

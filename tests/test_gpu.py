@@ -1033,17 +1033,18 @@ def test_gpu_bench_two_ranks_one_gpu(workload, tmp_path):
 
 # ---- closure tables in HBM (wide.hip): live width 25..31 -------------------
 
-@pytest.mark.parametrize("pipe", ["1", "0"])
+@pytest.mark.parametrize("pipe,grid", [("1", "0"), ("0", "0"), ("1", "8")])
 @pytest.mark.parametrize("minw", ["1", "12"])
-def test_gpu_wide_tables_vs_oracle(minw, pipe, monkeypatch):
+def test_gpu_wide_tables_vs_oracle(minw, pipe, grid, monkeypatch):
     """The HBM-table kernel, with LC_WIDE_MINW routing every history from that width on to it
     (in production it takes widths 25..31 only): random histories valid and invalid, 16-client
     histories with crashed ops, the low-slot orderings and tiny/empty ones, one launch for all
     of them, bit-exact with the oracle (verdict, failing op, its invocation, :previous-ok,
     explored). LC_WIDE_PIPE=1 (the default) overlaps consecutive steps on the grid, 0 runs one
-    step at a time."""
+    step at a time. LC_WIDE_GRID=8 runs the grid on 8 workgroups (the barrier's groups of one)."""
     monkeypatch.setenv("LC_WIDE_MINW", minw)
     monkeypatch.setenv("LC_WIDE_PIPE", pipe)
+    monkeypatch.setenv("LC_WIDE_GRID", grid)
     rng = random.Random(5)
     hs = [synth.gen_register(rng.randint(0, 60), rng.randint(1, 8), 0.2, 51000 + t, invalid=(t % 2 == 1))
           for t in range(120)]
