@@ -399,7 +399,7 @@ struct lc_plan {
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
-    plan_k16 = -1, plan_x = 1.57, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 13, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
+    plan_k16 = -1, plan_x = 1.2, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 12, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
     rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
     kfcap = klcap = 1 << 18;
     cell_cap = 256;
@@ -793,13 +793,16 @@ struct lc_plan {
   // sweep on C3: 0.4-0.45 -> 11.7 ms, 0.7 -> 13.4-13.6); a plan of a few histories is their
   // chain and keeps a higher factor (C2: 0.7 -> 35.5 ms, 0.4 -> 39.1 ms; rank shares: 1.0, r2cd).
   double plan_k16 = -1;  // < 0: 0.45 for a batch plan, else 1.0 (r2cd)
-  double plan_x = 1.57;  // LC_PLAN_X: the team model's cost per team bit (us per step)
+  // LC_PLAN_X: the team model's cost per team bit (us per step). Fitted at 1.57 (r2c-r2h); 1.2
+  // with a 12-slot floor (LC_PLAN_LBMIN) lets C2 take 12-slot tiles: 29.6 -> 28.1 ms, the 8-way C3
+  // shares, C3 and C4 unchanged (r3ag-r3ai)
+  double plan_x = 1.2;
   double plan_kb = 0.45;  // LC_PLAN_KB: the batch plan's VALU factor
   bool plan_rot = false;  // LC_PLAN_ROT: the team model knows which teams will be rotated
   // LC_PLAN_TM: a batch plan's team estimates times this (r3n LC_DEBUG: rotated 17-slot teams
   // took 1.3-1.8x their estimate while the BLOCK pool took 0.95x of its own)
   double plan_tm = 1.0;
-  int plan_lbmin = 13;  // LC_PLAN_LBMIN: the team planner's smallest tile (local slots)
+  int plan_lbmin = 12;  // LC_PLAN_LBMIN: the team planner's smallest tile (local slots)
   // A batch plan (LC_BATCH_HIST: more than 600 histories, e.g. C3 on one GPU) fills the chip,
   // so the launch is throughput-bound; fewer histories leave workgroups idle and the launch is
   // its slowest chain (r2rot6-8: C3 1000 keys 11.8 ms batch / 16.2 unrotated; a 250-key share
