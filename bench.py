@@ -545,7 +545,11 @@ def main():
     alg = fin * C + expl * (C + 8) + fout * C
     k_s = k_ms / 1e3
     achieved = alg / k_s / 1e9 if k_s > 0 else 0.0
-    prof = read_profile(args.traffic, args.workload, args.scale, kname)
+    tpath = args.traffic  # the other workloads' PMC summaries: profiles/traffic_latest_<workload>.json
+    alt = tpath.replace("traffic_latest.json", f"traffic_latest_{args.workload}.json")
+    if args.workload != "c3" and alt != tpath and os.path.exists(alt):
+        tpath = alt
+    prof = read_profile(tpath, args.workload, args.scale, kname)
     traffic = prof.get("hbm_bytes_per_launch") if prof else None
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,

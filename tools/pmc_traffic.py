@@ -46,7 +46,9 @@ def main(tag, fetch_csv, write_csv, workload, scale, kernel="dense_big_kernel", 
                 out[c.lower() + "_per_launch"] = v
         if "sq_insts_valu_per_launch" in out:
             out["valu_insts_per_launch"] = out["sq_insts_valu_per_launch"]
-    for name in (f"profiles/traffic_{tag}.json", "profiles/traffic_latest.json"):
+    # the headline (C3) keeps profiles/traffic_latest.json; other workloads get one file each
+    latest = "profiles/traffic_latest.json" if workload == "c3" else f"profiles/traffic_latest_{workload}.json"
+    for name in (f"profiles/traffic_{tag}.json", latest):
         json.dump(out, open(name, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
