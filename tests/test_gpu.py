@@ -1125,3 +1125,30 @@ def test_gpu_wide_tables_past_the_tile_teams():
     g = _lib.check(1, 0, h)
     assert _lib.check_stats()["wide_histories"] == 1
     assert int(g["valid"][0]) == 1 and int(g["explored"][0]) > 0
+
+
+def test_gpu_fuzz_register_and_counter_vs_oracle():
+    """Random histories of both models, one lc_check per model (the batch planner sees them all
+    together): 1-8 clients, 1-400 ops, 0-4 crashed writes/cas, :info on any op, valid and
+    perturbed, plus counters; bit-exact with the oracle. LC_FUZZ_N scales the register count
+    (default 200; r3ao ran 2000 on the GPU box, `profiles/r3ao`)."""
+    n = int(os.environ.get("LC_FUZZ_N", "200"))
+    rng = random.Random(71)
+    hs = []
+    for t in range(n):
+        hs.append(synth.gen_register(rng.randint(1, 400), rng.randint(1, 8), rng.choice([0.0, 0.01, 0.05]),
+                                     900000 + t, invalid=(t % 2 == 1),
+                                     n_crashed=rng.choice([None, 0, 1, 2, 4])))
+    h = H.concat(hs)
+    g = _lib.check(1, 0, h)
+    exp = oracle.check_many("cas-register", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, "fuzz register")
+    assert 0 < sum(e["valid"] == 0 for e in exp) < len(exp)
+    cs = [synth.gen_counter(rng.randint(1, 300), rng.randint(1, 8), 0.02, 910000 + t, invalid=(t % 3 == 2))
+          for t in range(max(20, n // 5))]
+    hc = H.concat(cs)
+    gc = _lib.check(2, 0, hc)
+    expc = oracle.check_many("counter", hc, n_threads=8)
+    for k in range(hc.n_hist):
+        _cmp(gc, expc[k], k, "fuzz counter")
