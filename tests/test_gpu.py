@@ -1152,3 +1152,23 @@ def test_gpu_fuzz_register_and_counter_vs_oracle():
     expc = oracle.check_many("counter", hc, n_threads=8)
     for k in range(hc.n_hist):
         _cmp(gc, expc[k], k, "fuzz counter")
+
+
+def test_gpu_fuzz_wide_register_vs_oracle():
+    """Wider random register histories in one lc_check: 12-16 clients, 100-400 ops, 0-5 crashed
+    writes/cas (live widths into the BLOCK, MID and tile-team classes, so the team planner's
+    12-slot tiles are in play), valid and perturbed; bit-exact with the oracle. LC_FUZZ_WIDE_N
+    scales it (default 60; r3ap ran 300 on the GPU box, `profiles/r3ap`)."""
+    n = int(os.environ.get("LC_FUZZ_WIDE_N", "60"))
+    rng = random.Random(73)
+    hs = [synth.gen_register(rng.randint(100, 400), rng.randint(12, 16), rng.choice([0.0, 0.01]), 930000 + t,
+                             invalid=(t % 2 == 1), n_crashed=rng.choice([0, 2, 4, 5])) for t in range(n)]
+    h = H.concat(hs)
+    widths = [_live_width(h, k) for k in range(h.n_hist)]
+    g = _lib.check(1, 0, h)
+    st = _lib.check_stats()
+    exp = oracle.check_many("cas-register", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"fuzz wide w={widths[k]}")
+    assert st["dense_histories"] == h.n_hist and max(widths) >= 17
+    assert any(e["valid"] == 0 for e in exp)
