@@ -374,6 +374,7 @@ struct lc_plan {
     if ((e = getenv("LC_TEAM_ROT"))) team_rot = std::max(-1, atoi(e));
     if ((e = getenv("LC_TEAM_ROT_LB"))) rot_min_lb = atoi(e);
     if ((e = getenv("LC_TEAM_ROT_CHAIN"))) rot_chain_lb = atoi(e);
+    if ((e = getenv("LC_TEAM_ROT_CHAIN_MIN"))) rot_chain_min = atoi(e);
     if ((e = getenv("LC_BATCH_HIST"))) batch_hist = atoi(e);
     if ((e = getenv("LC_MID_MAXW")) && atoi(e) > DENSE_WAVE_LMAX && atoi(e) <= DENSE_MID_LMAX) mid_maxw = atoi(e);
     if ((e = getenv("LC_TILE_WIDE")) && strchr(e, ':')) {
@@ -399,7 +400,7 @@ struct lc_plan {
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
-    plan_k16 = -1, plan_x = 1.2, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 12, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, batch_hist = 600, mid_maxw = 0;
+    plan_k16 = -1, plan_x = 1.2, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 12, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, rot_chain_min = 14, batch_hist = 600, mid_maxw = 0;
     rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
     kfcap = klcap = 1 << 18;
     cell_cap = 256;
@@ -779,6 +780,7 @@ struct lc_plan {
   int team_rot = -1;       // LC_TEAM_ROT: tile-team slot rotation (build_dense; -1 auto)
   int rot_min_lb = 16;     // LC_TEAM_ROT_LB: auto rotation from this tile size
   int rot_chain_lb = 14;   // LC_TEAM_ROT_CHAIN: a chain plan's teams of this tile size (>= 4 team bits)
+  int rot_chain_min = 14;  // LC_TEAM_ROT_CHAIN_MIN: ... and of the smaller tile sizes down to this one
   // rotation keeps slots 0..2 in the word (the encoder's slot policy; LC_SLOTS=lff: rotate them too)
   bool rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
   // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7); by default 14 for
@@ -816,7 +818,7 @@ struct lc_plan {
     int wide = 0;
     for (int L = lb + 1; L <= 32; ++L) wide += (int)ws.c[L];
     const bool mostly_wide = 10 * wide >= 4 * (int)ws.steps();
-    const bool chain_widest = !batch_plan() && lb == rot_chain_lb && lw - lb >= 4;
+    const bool chain_widest = !batch_plan() && lb <= rot_chain_lb && lb >= std::min(rot_chain_min, rot_chain_lb) && lw - lb >= 4;
     return chain_widest || (lb >= rot_min_lb && (batch_plan() || mostly_wide));
   }
   // lw: the history's widest step. A rotated team (LC_PLAN_ROT, r3) has its t = lw - lb team
