@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 # MI355X_MICROARCH.md §LDS: ds_read_b64 moves 256 B/clk/CU; 256 CUs at 2.4 GHz
 LDS_PEAK_GBS = 256 * 256 * 2.4
 MODEL_OF = {"c1": "cas-register", "c2": "cas-register", "c3": "cas-register",
-            "c4": "cas-register", "c5": "counter"}
+            "c4": "cas-register", "c5": "counter", "c2c": "counter", "c5x": "counter"}
 
 
 # one process per GPU over RCCL ("nccl"); LC_BENCH_BACKEND=gloo and LC_BENCH_DEVICE=<index> are
@@ -51,17 +51,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = False):
-    """Time the CPU oracle (a C restatement of knossos.linear, test infrastructure) on a
-    bounded, FIXED sample of the same workload; returns (cpu dict, oracle results, sample
-    keys, sampled history).
+def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = True):
+    """Time the CPU oracle (a C restatement of knossos.linear, test infrastructure) on the
+    same workload in the same run; returns (cpu dict, oracle results, checked keys, checked
+    history).
 
-    Many keys: every 20th key (0, 20, ..., 980 for C3: 50 keys, ~20 s of CPU work), checked by
-    `threads` POSIX threads that take keys from a shared counter (dynamic scheduling). The
-    sample does not depend on a timing probe, so two runs check the same keys; the per-key
-    wall times come back from the oracle. `full` checks every key (the whole workload: minutes
-    on C3, whose two heaviest keys take ~2 min each on one core). One history: the longest
-    prefix that fits the budget (the oracle is single-threaded per history, as Knossos is)."""
+    Many keys (r4): EVERY key by default — the whole workload, checked by
+    `threads` POSIX threads that take keys in key order from a shared counter (dynamic
+    scheduling), as Knossos would check them; on C3 that is ~50 s on the GPU box's 16 threads
+    (~200 s of CPU work; the wall is the slowest key's single-thread search plus the work
+    dequeued before it). The work is a fixed set of deterministic searches, so two runs differ
+    only by the machine. `value` is the wall figure; `per_key_sum` beside it is the throughput
+    if the per-key times packed perfectly onto the threads (sum / threads). full=False: every
+    20th key (a quick sample whose wall is one key's time; not a baseline to quote). One
+    history: the longest prefix that fits the budget (the oracle is single-threaded per
+    history, as Knossos is)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (bench cpu_baseline leg only)
     n = h.n_hist
@@ -73,14 +77,15 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = Fals
         res = oracle.check_many(model, hs, n_threads=threads)
         wall = time.perf_counter() - t0
         per = np.array([r["wall_ns"] for r in res], np.float64) / 1e9
-        desc = (f"all {n} keys" if full or stride == 1 else
-                f"every {stride}th key ({len(sample)} of {n}: 0, {stride}, ...)") + \
-            f", {threads} threads taking keys from a shared counter"
+        desc = (f"the whole workload: all {n} keys" if full or stride == 1 else
+                f"every {stride}th key ({len(sample)} of {n}: 0, {stride}, ...; a quick sample)") + \
+            f", {threads} threads taking keys in key order from a shared counter"
         used = threads
         keys = {"min_s": round(float(per.min()), 5), "median_s": round(float(np.median(per)), 5),
                 "max_s": round(float(per.max()), 4), "sum_s": round(float(per.sum()), 4),
                 "slowest_key": int(sample[int(per.argmax())]),
-                "ops_per_s_if_perfectly_packed": ops_of(hs) / max(float(per.sum()) / threads, 1e-9)}
+                "ops_per_s_if_perfectly_packed": ops_of(hs) / max(float(per.sum()) / threads, 1e-9),
+                "wall_bound_s": round(max(float(per.sum()) / threads, float(per.max())), 3)}
     else:
         # one history: the oracle is single-threaded like Knossos's per-history search;
         # time the longest prefix that fits the budget, growing from a short one (a wide
@@ -111,22 +116,6 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = Fals
 
 def ops_of(h):
     return h.n_ops()
-
-
-def whole_workload_cpu(path, workload, threads):
-    """The committed whole-workload CPU run (bench.py --cpu-full on a GPU box, kept under
-    profiles/) for this workload at this thread count, or None."""
-    if not os.path.exists(path):
-        return None
-    try:
-        d = json.load(open(path))
-    except Exception:  # noqa: BLE001
-        return None
-    cb = d.get("cpu_baseline") or {}
-    if not d.get("config", {}).get("workload", "").startswith(workload + ":") or cb.get("cores") != threads:
-        return None
-    return {"value": cb.get("value"), "wall_s": cb.get("wall_s"), "per_key": cb.get("per_key"),
-            "cpu_model": cb.get("cpu_model"), "source": os.path.relpath(path, ROOT)}
 
 
 def bench_c5(args, rank, world, dist, barrier_sync):
@@ -383,10 +372,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=6.0,
                     help="CPU baseline sizing (the 16-key probe underestimates the sample ~2.5x: ~15 s)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-full", action="store_true",
-                    help="cpu_baseline on every key (the whole workload; minutes on C3)")
-    ap.add_argument("--cpu-whole", default=os.path.join(ROOT, "profiles", "cpu_whole_c3.json"),
-                    help="committed --cpu-full run quoted as cpu_baseline.whole_workload")
+    ap.add_argument("--cpu-sample", action="store_true",
+                    help="cpu_baseline on every 20th key only (quick; the default is every key)")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="lc_check calls from host arrays timed after the run (0: skip)")
     ap.add_argument("--emulate", default="",
@@ -525,7 +512,12 @@ def main():
         for k, v in s_.items():
             acc[k] = acc.get(k, 0.0) + v
     avg = {k: v / args.steps for k, v in acc.items()}
-    if st["dense_histories"] > 0:
+    if st.get("ctab_histories", 0) > 0:
+        kname = "lc::ctab_kernel"
+        k_ms = avg["ctab_ms"]
+        fin, fout, expl = avg["ctab_frontier_in"], avg["ctab_frontier_out"], avg["ctab_explored"]
+        table_hbm = lds_bytes = None
+    elif st["dense_histories"] > 0:
         which = "big" if avg["dense_big_ms"] >= avg["dense_wave_ms"] else "wave"
         kname = f"lc::dense_{which}_kernel"
         k_ms = avg[f"dense_{which}_ms"]
@@ -580,26 +572,25 @@ def main():
     parity = None
     if not args.no_cpu and world == 1 and not args.emulate:
         ci = cpu_info()
-        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, ci["threads"], args.cpu_full)
+        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, ci["threads"], not args.cpu_sample)
         cpu.update({k: ci[k] for k in ("cpu_model", "nproc", "affinity")})
         cpu["cores_from"] = ci["share"]
         if h.n_hist > 1:
-            # the GPU/CPU ratio on the same keys (GPU: the whole workload's check, which
-            # includes these keys; a lower bound on the GPU's speed over the sample)
-            cpu["gpu_over_cpu_same_keys"] = value / cpu["value"]
-            whole = whole_workload_cpu(args.cpu_whole, args.workload, ci["threads"])
-            if whole and whole.get("value"):
-                whole["gpu_over_cpu"] = value / whole["value"]
-                pk = whole.get("per_key") or {}
-                if pk.get("sum_s") and pk.get("max_s"):
-                    # every core this process may use (affinity), from the measured per-key
-                    # times: the wall is at least max(sum / cores, the slowest key) (projection)
-                    whole["projected_all_affinity"] = {
-                        "cores": ci["affinity"],
-                        "value": h.n_ops() / max(pk["sum_s"] / ci["affinity"], pk["max_s"]),
-                        "note": "projection from per-key times, not measured (the box's CPU "
-                                "share is 16 threads)"}
-            cpu["whole_workload"] = whole
+            # the GPU/CPU ratio from the same run, over the same keys
+            cpu["gpu_over_cpu"] = value / cpu["value"]
+            pk = cpu.get("per_key") or {}
+            if pk.get("sum_s"):
+                cpu["per_key_sum"] = {"value": pk["ops_per_s_if_perfectly_packed"],
+                                      "gpu_over_cpu": value / pk["ops_per_s_if_perfectly_packed"],
+                                      "note": "history ops / (sum of per-key times / threads): the "
+                                              "CPU throughput if the keys packed perfectly"}
+                # every core this process may use (affinity), from the measured per-key times:
+                # the wall is at least max(sum / cores, the slowest key) (projection)
+                cpu["projected_all_affinity"] = {
+                    "cores": ci["affinity"],
+                    "value": hs.n_ops() / max(pk["sum_s"] / ci["affinity"], pk["max_s"]),
+                    "note": "projection from per-key times, not measured (the box's CPU share is "
+                            f"{ci['threads']} threads)"}
         if h.n_hist > 1:
             mism = [k for i, k in enumerate(sample)
                     if int(res["valid"][k]) != ores[i]["valid"] or
@@ -615,7 +606,9 @@ def main():
     desc = {"c1": "register 10 keys x 200 ops, 5 clients",
             "c2": "register 1 key x 5k ops, 16 clients",
             "c3": "jepsen.independent cas-register 1k keys x 1k ops, 5 clients/key",
-            "c4": "register 1 key x 100k ops, 16 clients, crashed :info ops"}[args.workload]
+            "c4": "register 1 key x 100k ops, 16 clients, crashed :info ops",
+            "c2c": "counter 1 key x 5k ops, 16 clients (C2's shape), one whole-history search",
+            "c5x": "counter 1M ops, 16 clients, 4 crashed ops (C5's exact-search variant)"}[args.workload]
     out = {
         "metric": "history ops verified/sec (+ configs explored/sec, % HBM roofline)",
         "value": value,

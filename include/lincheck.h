@@ -54,6 +54,9 @@ enum lc_hist_error {
   LC_H_WIDE = -5,       /* more concurrently pending ops than the packed key holds */
   LC_H_MODEL = -6,      /* op the model cannot step (unknown :f, wrong value shape, overflow) */
   LC_H_CAPACITY = -7,   /* frontier/closure exceeded max_configs or device capacity */
+  LC_H_ABORTED = -8,    /* a device-wide search was stopped by its barrier watchdog (its grid was not
+                           wholly resident: another user of the device); undecided, the other
+                           histories of the call keep their answers */
 };
 /* flags */
 #define LC_FLAG_BOUNDS_ONLY 0x1 /* counter: run only the bounds pre-filter (sound rejection) */
@@ -99,7 +102,8 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist,
  * lc_check keeps one plan per device between calls (device buffers sized to the largest check
  * so far, streams, occupancy). lc_release frees the cached plan of `device` (< 0: every
  * device) and its device memory; the next lc_check rebuilds it. A long-lived caller (the JVM)
- * calls it after a large check; it is never done by a static destructor at process exit.
+ * calls it after a large check; it is never done by a static destructor at process exit. It
+ * also frees the calling thread's host encoder buffers (kept between that thread's calls).
  * Not part of the reference interface (Knossos keeps no device state).
  */
 int32_t lc_release(int32_t device);
@@ -215,8 +219,10 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  * 31 histories decided on closure tables in HBM (wide.hip: live width 25..31; counted in 12 too)
  * 32 their kernel's ms (part of 0 and 13)
  * 33 their algorithmic HBM bytes: per step and live word, its X, its pulls and its store (8 B each)
+ * 34 counter histories decided on closure tables (ctab.hip; counted in 12 too)  35 their kernel's ms
+ * 36..38 the counter tables' frontier configs in, frontier configs out, configs explored
  */
-#define LC_STATS_N 34
+#define LC_STATS_N 39
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
 void lc_plan_destroy(lc_plan* p);
 

@@ -31,7 +31,8 @@
 
 (def ^:private err-text
   {-4 "malformed history" -5 "too many concurrently pending ops"
-   -6 "model cannot step an op" -7 "frontier exceeded max-configs / device capacity"})
+   -6 "model cannot step an op" -7 "frontier exceeded max-configs / device capacity"
+   -8 "device search aborted by its barrier watchdog (device not wholly available)"})
 
 (defn- c-string [^bytes buf]
   (String. buf 0 (int (or (first (keep-indexed #(when (zero? %2) %1) buf)) (alength buf)))))

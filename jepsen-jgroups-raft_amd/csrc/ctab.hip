@@ -1,0 +1,446 @@
+// ctab.hip — counter closure tables (see ctab.hpp): knossos.linear/analysis [ext] (SURVEY §8(a)
+// a5) with CounterModel.step (a7, src/jepsen/jgroups/workload/counter.clj:100-127) applied to
+// whole bitmaps of configs, one history per 1024-thread workgroup, the table in LDS.
+//
+// One RETURN step of slot j on table B (bit (w, p) = "the config with mask (w << 6) | p exists";
+// R = configs produced by a consistent step, X = the frontier before the step):
+//   for hi-layer q = 0..H (words w of popcount q over the live slots >= 6), in parallel:
+//     j hi and j ∈ w : R = B[w \ j] & G_j(w \ j)           (configs holding j are never expanded)
+//     otherwise      : R = ∪_{b ∈ w} B[w \ b] & G_b(w \ b)   (pulls from finished words)
+//                      then the in-word closure over the live low slots k != j (each op's gated
+//                      transfer (X | R) & G_k moved up by 2^k, repeated until nothing changes)
+//                      and, when j is a low slot, one final j transfer
+//     explored += popcount(R);  B[w] = X | R
+//   return j: B'[m] = B[m ∪ j] for m ∌ j                   B' empty => invalid at this RETURN
+// G_k(v) = the positions p of word v whose config may step op k: every position for an
+// unconstrained op, else those with S_lo(p) = req_k - base - S_hi(v) (an EQ lookup), minus the
+// positions holding k (and j: configs holding the returning op are never expanded).
+// Every config reachable by linearizing pending calls is produced at exactly its own mask,
+// whose predecessors are final earlier, so R is the sparse search's closure set and
+// popcount(R) its explored count, bit-exact with the oracle.
+//
+// Steps are pipelined as the register tables' history_pipe (dense.hip): step t's
+// layer q runs in the same super-layer as step t-1's layer q + 2 (q + 1 after an in-word return
+// on double-buffered tables); one workgroup barrier ends a super-layer; step t reads its
+// frontier X through step t-1's returning slot from step t-1's table, so the return is never
+// applied in place. A ring of decoded steps holds each step's per-slot requirements, its EQ
+// table and its hi-slot delta sums.
+#include "ctab.hpp"
+#include "dense.hpp"
+#include "search.hpp"
+
+namespace lc {
+namespace {
+
+constexpr int CT_TEAM = 1024;
+constexpr int CT_RING = 16;
+constexpr int CT_CAPW = 1 << (CTAB_LMAX - CTAB_LO);  // LDS table words (128 KiB)
+constexpr int CT_BINOM = 24;
+constexpr int32_t CQ_UNC = 0x3fffffff;   // cq sentinel: the op steps from any config
+constexpr int32_t CQ_NEVER = -0x3fffffff;  // ... from none (out of the EQ range whatever the sum)
+constexpr int CT_PIPE_DBL = 1;
+
+struct __attribute__((aligned(16))) CStep {
+  uint32_t live, fresh, anyx;
+  int32_t base;              // sum of the deltas of the ops returned before this step
+  int32_t j, jp, H, start;   // returning slot, previous step's, layers - 1, first super-layer
+  uint64_t keep_lo;          // positions without a fresh low slot
+  int32_t req[32];           // per slot: requirement relative to init (CQ_UNC / CQ_NEVER)
+  int32_t cq[32];            // per slot: EQ index base (k < 6: req - base - lo_min; k >= 6: + d_k)
+  int8_t d[32];              // per slot: delta
+  int16_t sh[2][128];        // sums of the hi slots' deltas: slots 6..12 by w & 127, 13..19 by w >> 7
+  uint64_t eq[64];           // EQ[v]: positions p with S_lo(p) - lo_min = v
+};
+
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <typename T>
+__device__ __forceinline__ T rdl(T v, int l) {
+  return (T)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// positions (of 64) whose mask lacks low slot k
+__device__ __forceinline__ uint64_t keep6(int k) {
+  switch (k) {
+    case 0: return 0x5555555555555555ull;
+    case 1: return 0x3333333333333333ull;
+    case 2: return 0x0f0f0f0f0f0f0f0full;
+    case 3: return 0x00ff00ff00ff00ffull;
+    case 4: return 0x0000ffff0000ffffull;
+    default: return 0x00000000ffffffffull;
+  }
+}
+
+__device__ __forceinline__ uint64_t gate(const CStep* st, int32_t c, int s) {
+  if (c == CQ_UNC) return ~0ull;
+  const uint32_t i = (uint32_t)(c - s);
+  return i < 64u ? st->eq[i] : 0ull;
+}
+
+// per-wave window of 128 words over a history's step stream: lane i holds words base + i and
+// base + 64 + i (a step is at most 1 + 2 * CTAB_MAX_NINV = 63 words)
+struct StreamWin {
+  int64_t base = -(1ll << 40);
+  uint32_t w0 = 0, w1 = 0;
+  __device__ __forceinline__ void need(const CtabParams& p, int64_t pos, int lane) {
+    if (pos + 64 > base + 128) {
+      base = pos;
+      w0 = (base + lane < p.stream_words) ? p.stream[base + lane] : 0u;
+      w1 = (base + 64 + lane < p.stream_words) ? p.stream[base + 64 + lane] : 0u;
+    }
+  }
+  __device__ __forceinline__ uint32_t at(int64_t pos) const {
+    const int off = (int)(pos - base);
+    const uint32_t a = (uint32_t)__shfl((int)w0, off & 63, 64), b = (uint32_t)__shfl((int)w1, off & 63, 64);
+    return off < 64 ? a : b;
+  }
+};
+
+// Decode the step at pos into dst (one whole wave): the per-slot requirements and deltas are
+// the previous step's plus this step's invocations; then the derived tables (cq, EQ, hi sums).
+__device__ __forceinline__ void ct_decode(const CtabParams& p, StreamWin& sw, int64_t& pos, int lane, CStep* dst,
+                                          const CStep* prev) {
+  sw.need(p, pos, lane);
+  const uint32_t H0 = (uint32_t)rfl((int)sw.at(pos));
+  const uint32_t wd = sw.at(pos + 1 + lane);
+  const int nw = (int)__builtin_ctzll(~__ballot(lane < 2 * CTAB_MAX_NINV && (wd & DENSE_OPW)));
+  const int ninv = nw >> 1;
+  const uint32_t w0 = sw.at(pos + 1 + 2 * lane), w1 = sw.at(pos + 2 + 2 * lane);
+  // lane k < 32: slot k's requirement and delta after this step's invocations
+  int32_t req = prev && lane < 32 ? prev->req[lane] : CQ_UNC;
+  int32_t d = prev && lane < 32 ? (int32_t)prev->d[lane] : 0;
+  for (int i = 0; i < ninv; ++i) {
+    const uint32_t a = (uint32_t)rdl((int)w0, i), b = (uint32_t)rdl((int)w1, i);
+    if (lane == (int)(a & 31u)) {
+      const uint32_t fl = (a >> 8) & 0xffu;
+      d = (int32_t)(int8_t)(uint8_t)((a >> 16) & 0xffu);
+      req = (fl & CT_UNC) ? CQ_UNC : (fl & CT_NEVER) ? CQ_NEVER : (int32_t)(b & 0x3fffffffu) - CTAB_REQ_BIAS;
+    }
+  }
+  const uint32_t plive = prev ? (uint32_t)rfl((int)prev->live) : 0u;
+  const int pj = prev ? rfl(prev->j) : -1;
+  const int32_t base = prev ? rfl(prev->base) + (int32_t)prev->d[pj] : 0;
+  // low sums: lane p = the sum of the deltas of p's slots; lo_min = the smallest
+  int32_t slo = 0, lo_min = 0;
+#pragma unroll
+  for (int k = 0; k < CTAB_LO; ++k) {
+    const int32_t dk = rdl(d, k);
+    if ((lane >> k) & 1) slo += dk;
+    lo_min += dk < 0 ? dk : 0;
+  }
+  if (lane < 32) {
+    dst->req[lane] = req;
+    dst->d[lane] = (int8_t)d;
+    dst->cq[lane] = req == CQ_UNC || req == CQ_NEVER ? req : req - base - lo_min + (lane >= CTAB_LO ? d : 0);
+  }
+  dst->eq[lane] = 0;
+  // (one wave's LDS operations stay in order: the zeroing lands before the ORs)
+  __hip_atomic_fetch_or(&dst->eq[slo - lo_min], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // hi sums: entries lane and lane + 64 of both halves
+#pragma unroll
+  for (int half = 0; half < 2; ++half)
+#pragma unroll
+    for (int e2 = 0; e2 < 2; ++e2) {
+      const int e = lane + 64 * e2;
+      int32_t s = 0;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const int32_t dk = rdl(d, CTAB_LO + 7 * half + k);
+        if ((e >> k) & 1) s += dk;
+      }
+      dst->sh[half][e] = (int16_t)s;
+    }
+  if (lane == 0) {
+    const uint32_t live = H0 & DENSE_LIVE_MASK;
+    const int L = live ? 32 - __clz((int)live) : 0;
+    const uint32_t fresh = prev ? live & ~(plive & ~(1u << pj)) : live;
+    uint64_t kl = ~0ull;
+    for (int k = 0; k < CTAB_LO; ++k)
+      if (fresh & (1u << k)) kl &= keep6(k);
+    dst->live = live;
+    dst->fresh = fresh;
+    dst->anyx = 0;
+    dst->base = base;
+    dst->j = (int)((H0 >> DENSE_J_SHIFT) & 31u);
+    dst->jp = pj;
+    dst->H = L > CTAB_LO ? L - CTAB_LO : 0;
+    dst->start = 1 << 30;  // not started
+    dst->keep_lo = kl;
+  }
+  pos += 1 + nw;
+}
+
+// word w's frontier before step (fresh, jp): step jp's post-return table, read in place
+__device__ __forceinline__ uint64_t ct_x(const uint64_t* B, uint32_t w, uint32_t fresh_hi, int jp, uint64_t keep_lo) {
+  if (w & fresh_hi) return 0;
+  uint64_t v;
+  if (jp >= CTAB_LO) v = B[w | (1u << (jp - CTAB_LO))];
+  else if (jp >= 0) v = (B[w] & ~keep6(jp)) >> (1 << jp);
+  else v = B[w];
+  return v & keep_lo;
+}
+
+// One step's closure of word w (its frontier X): the hi pulls and the in-word closure. Returns R.
+__device__ __forceinline__ uint64_t ct_word(const uint64_t* Bt, uint32_t w, const CStep* st, uint32_t live, int j,
+                                            uint64_t X) {
+  const int s_hi = (int)st->sh[0][w & 127u] + (int)st->sh[1][(w >> 7) & 127u];
+  const bool jhi = j >= CTAB_LO;
+  const uint32_t jh = jhi ? 1u << (j - CTAB_LO) : 0u;
+  uint32_t m = (w & jh) ? jh : w;
+  uint64_t R = 0;
+  while (m) {  // the word's set hi bits, two at a time (their loads issued together)
+    int b[2];
+    uint64_t v[2];
+    int32_t c[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      b[u] = m ? __builtin_ctz(m) : -1;
+      m &= m - 1;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      v[u] = b[u] >= 0 ? Bt[w ^ (1u << b[u])] : 0ull;
+      c[u] = b[u] >= 0 ? st->cq[CTAB_LO + b[u]] : CQ_NEVER;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) R |= v[u] & gate(st, c[u], s_hi);
+  }
+  if (w & jh) return R;  // a word holding j (hi) is produced by linearizing j last only
+  const uint64_t notj = jhi ? ~0ull : keep6(j);
+  R &= notj;
+  const uint32_t lo = live & 63u & ~(jhi ? 0u : 1u << j);
+  uint64_t G[CTAB_LO];
+#pragma unroll
+  for (int k = 0; k < CTAB_LO; ++k) G[k] = ((live >> k) & 1u) ? gate(st, st->cq[k], s_hi) & keep6(k) & notj : 0ull;
+  for (;;) {  // the in-word closure: gated transfers until nothing changes
+    const uint64_t R0 = R;
+#pragma unroll
+    for (int k = 0; k < CTAB_LO; ++k)
+      if ((lo >> k) & 1u) R |= ((X | R) & G[k]) << (1 << k);
+    if (R == R0) break;
+  }
+  if (!jhi) {  // the returning op, linearized last
+#pragma unroll
+    for (int k = 0; k < CTAB_LO; ++k)
+      if (k == j) R |= ((X | R) & G[k]) << (1 << k);
+  }
+  return R;
+}
+
+__device__ __forceinline__ void init_binom(uint32_t* binom, int tid, int nthreads) {
+  for (int i = tid; i < CT_BINOM * CT_BINOM; i += nthreads) {
+    const int n = i / CT_BINOM, k = i % CT_BINOM;
+    uint32_t c = 0;
+    if (k <= n) {
+      uint64_t v = 1;
+      for (int q = 1; q <= k; ++q) v = v * (uint64_t)(n - k + q) / (uint64_t)q;
+      c = (uint32_t)v;
+    }
+    binom[i] = c;
+  }
+}
+
+__global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
+  __shared__ uint64_t sTab[CT_CAPW];
+  __shared__ CStep sRing[CT_RING];
+  __shared__ uint32_t sBinom[CT_BINOM * CT_BINOM];
+  __shared__ uint32_t sWOff[CT_BINOM + 2];
+  __shared__ int sQ;
+  __shared__ unsigned long long sExpl;
+  const int tt = threadIdx.x, lane = tt & 63;
+  const bool decoder = tt >= CT_TEAM - 64;  // the last wave: packed passes fill the low threads first
+  init_binom(sBinom, tt, CT_TEAM);
+  if (tt <= DENSE_WORD_BITS + 1) {  // offsets of the global list's popcount layers
+    uint32_t o = 0;
+    for (int q = 0; q < tt; ++q) {
+      uint64_t v = 1;
+      for (int i = 1; i <= q; ++i) v = v * (uint64_t)(DENSE_WORD_BITS - q + i) / (uint64_t)i;
+      o += (uint32_t)v;
+    }
+    sWOff[tt] = o;
+  }
+  __syncthreads();
+  unsigned long long st_fout = 0, st_steps = 0;
+  for (;;) {
+    if (tt == 0) sQ = atomicAdd(p.queue, 1), sExpl = 0;
+    __syncthreads();
+    const int qi = sQ;
+    if (qi >= p.n) break;
+    const int h = p.order[qi];
+    if (p.stamps && tt == 0) p.stamps[2 * h] = __builtin_amdgcn_s_memrealtime();
+    const int lmax = p.lmax[h];
+    const int ns = p.nsteps[h];
+    const int Hh = lmax > CTAB_LO ? lmax - CTAB_LO : 0;
+    const int NW = 1 << Hh;
+    const bool dbl = (p.pipe & CT_PIPE_DBL) && 2 * NW <= CT_CAPW;
+    uint64_t* const B = sTab;
+    uint64_t* const B2 = dbl ? sTab + NW : sTab;
+    auto tab = [&](int t) { return (t & 1) ? B2 : B; };
+    const int ntab = dbl ? 2 * NW : NW;
+    for (int i = tt; i < ntab; i += CT_TEAM) sTab[i] = 0;
+    // the word list in the LDS left beside the tables (layers of the Hh-bit words), else global
+    const uint32_t* words = p.words;
+    const uint32_t* wofs = sWOff;
+    uint32_t* const lw = reinterpret_cast<uint32_t*>(sTab + ntab);
+    uint32_t* const lo = lw + NW;
+    const bool lds_list = Hh > 0 && ntab + NW / 2 + 16 <= CT_CAPW;
+    if (lds_list) {
+      if (tt <= Hh + 1) {
+        uint32_t o = 0;
+        for (int q = 0; q < tt; ++q) o += sBinom[Hh * CT_BINOM + q];
+        lo[tt] = o;
+      }
+      __syncthreads();
+      for (int q = 0; q <= Hh; ++q) {
+        const uint32_t nq = sBinom[Hh * CT_BINOM + q], og = sWOff[q], ol = lo[q];
+        for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)CT_TEAM) lw[ol + r] = p.words[og + r];
+      }
+      words = lw, wofs = lo;
+    }
+    __syncthreads();
+    if (tt == 0) B2[0] = 1;  // the initial config: nothing linearized (step 0 reads tab(-1))
+    StreamWin sw;
+    int64_t pos = p.sbeg[h];
+    if (ns > 0 && decoder) {
+      ct_decode(p, sw, pos, lane, &sRing[0], nullptr);
+      if (lane == 0) sRing[0].start = 0;
+    }
+    __syncthreads();
+    unsigned long long expl = 0;
+    int fail_t = -1;
+    int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0;  // decoded, started, retired
+    for (int s = 0; t_ret < ns; ++s) {
+      // ---- ring view: lane i = step t_ret + i (decoded steps only)
+      const int tl = t_ret + lane;
+      const bool dec_l = lane < CT_RING && tl < t_dec;
+      uint4 h0 = {0u, 0u, 0u, 0u};
+      int4 h1 = {0, 0, 0, 1 << 30};
+      if (dec_l) {
+        const CStep* st = &sRing[tl % CT_RING];
+        h0 = *reinterpret_cast<const uint4*>(&st->live);  // live, fresh, anyx, base
+        h1 = *reinterpret_cast<const int4*>(&st->j);      // j, jp, H, start
+      }
+      const bool run_l = dec_l && tl < t_run;
+      // retire the steps whose last layer ran in an earlier super-layer, in order
+      const bool fin_l = run_l && h1.w + h1.z < s;
+      const uint64_t fin = __ballot(fin_l);
+      const int lead = (int)__builtin_ctzll(~fin);
+      const uint64_t lead_mask = lead >= 64 ? ~0ull : (1ull << lead) - 1;
+      const uint64_t bad = __ballot(fin_l && tl > 0 && h0.z == 0u) & lead_mask;
+      if (bad) {  // step (first such) - 1 returned an empty frontier
+        fail_t = t_ret + (int)__builtin_ctzll(bad) - 1;
+        break;
+      }
+      const int t_ret_old = t_ret;
+      t_ret += lead;
+      if (t_ret >= ns) break;
+      // ---- segments: running steps in their layer q = s - start <= H
+      const int q_l = s - h1.w;
+      const bool seg_l = run_l && q_l >= 0 && q_l <= h1.z;
+      uint32_t nq_l = 0, o_l = 0;
+      if (seg_l) nq_l = sBinom[h1.z * CT_BINOM + q_l], o_l = wofs[q_l];
+      const uint64_t segm = __ballot(seg_l);
+      // the segments' words packed over the team, each padded to whole waves (every wave works
+      // on a single step: its parameters are wave-uniform)
+      uint32_t total = 0;
+      for (uint64_t m = segm; m; m &= m - 1) total += (rdl(nq_l, (int)__builtin_ctzll(m)) + 63u) & ~63u;
+      for (uint32_t f0 = (uint32_t)(tt & ~63); f0 < total; f0 += (uint32_t)CT_TEAM) {
+        int i = 0;
+        uint32_t e = 0, acc = 0;
+        for (uint64_t m = segm; m; m &= m - 1) {
+          const int k = (int)__builtin_ctzll(m);
+          if (f0 >= acc) i = k, e = acc;
+          acc += (rdl(nq_l, k) + 63u) & ~63u;
+        }
+        const uint32_t nq = rdl(nq_l, i), r = f0 - e + (uint32_t)lane;
+        const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i);
+        const int j = rdl(h1.x, i), jp = rdl(h1.y, i);
+        const int t = t_ret_old + i;
+        if (r >= nq) continue;
+        const uint32_t w = words[rdl(o_l, i) + r];
+        if (w & ~(live >> CTAB_LO)) continue;
+        CStep* st = &sRing[t % CT_RING];
+        uint64_t* const Bt = tab(t);
+        const uint64_t X = ct_x(tab(t - 1), w, fresh >> CTAB_LO, jp, st->keep_lo);
+        const uint64_t R = ct_word(Bt, w, st, live, j, X);
+        Bt[w] = X | R;
+        expl += (uint32_t)__popcll(R);
+        if (t > 0) st_fout += (uint32_t)__popcll(X);
+        if (X) st->anyx = 1;
+      }
+      // ---- decode ahead into a slot nobody read in this super-layer
+      const int t_dec_old = t_dec;
+      if (t_dec < ns && t_dec - t_ret_old < CT_RING) {
+        if (decoder) ct_decode(p, sw, pos, lane, &sRing[t_dec % CT_RING], &sRing[(t_dec - 1) % CT_RING]);
+        ++t_dec;
+      }
+      // ---- start the next decoded step at s + 1: two super-layers after its predecessor (one
+      // if that has a single layer, or returned an in-word slot on double-buffered tables), or
+      // at once if the predecessor retired
+      if (t_run < t_dec_old) {
+        const int lp = t_run - 1 - t_ret_old;  // the predecessor's lane (< 0: retired)
+        bool ok;
+        if (lp < 0 || lp < lead) {
+          ok = true;
+        } else {
+          const bool pred_hi = rdl(h1.x, lp) >= CTAB_LO;
+          const int gap = (dbl && !pred_hi) ? 1 : 2;
+          ok = s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h1.z, lp) + 1);
+        }
+        if (ok) {
+          if (tt == 0) sRing[t_run % CT_RING].start = s + 1;
+          ++t_run;
+        }
+      }
+      __syncthreads();
+    }
+    if (fail_t < 0 && ns > 0) {  // the last step's return
+      const CStep* st = &sRing[(ns - 1) % CT_RING];
+      const int jl = rfl(st->j);
+      const uint32_t live = (uint32_t)rfl((int)st->live) & ~(1u << jl);
+      const int L = live ? 32 - __clz((int)live) : 0;
+      const int nwt = 1 << (L > CTAB_LO ? L - CTAB_LO : 0);
+      uint64_t nzx = 0;
+      for (int w = tt; w < nwt; w += CT_TEAM) {
+        if ((uint32_t)w & ~(live >> CTAB_LO)) continue;
+        const uint64_t X = ct_x(tab(ns - 1), (uint32_t)w, 0u, jl, ~0ull);
+        st_fout += (uint32_t)__popcll(X);
+        nzx |= X;
+      }
+      if (!__syncthreads_or(nzx != 0)) fail_t = ns - 1;
+    }
+    if (tt == 0) st_steps += fail_t >= 0 ? fail_t + 1 : ns;
+    for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
+    if (lane == 0 && expl) atomicAdd(&sExpl, expl);
+    __syncthreads();
+    if (tt == 0) {
+      p.explored[h] = sExpl;
+      p.fail_step[h] = fail_t;
+      p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      if (p.stamps) p.stamps[2 * h + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+    __syncthreads();
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    st_fout += __shfl_down(st_fout, off, 64);
+    st_steps += __shfl_down(st_steps, off, 64);
+  }
+  if (lane == 0 && st_fout) atomicAdd(&p.stats[0], st_fout);
+  if (lane == 0 && st_steps) atomicAdd(&p.stats[1], st_steps);
+}
+
+}  // namespace
+
+int ctab_grid_size() {
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ctab_kernel, CT_TEAM, 0) != hipSuccess) return 0;
+  return ncu * per;
+}
+
+hipError_t launch_ctab(const CtabParams& p, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(ctab_kernel, dim3(grid), dim3(CT_TEAM), 0, stream, p);
+  return hipGetLastError();
+}
+
+}  // namespace lc

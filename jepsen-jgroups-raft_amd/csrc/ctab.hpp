@@ -1,0 +1,62 @@
+// ctab.hpp — closure-table search for counter histories.
+//
+// The reference checks a counter run as ONE whole-history knossos.linear search with
+// CounterModel (src/jepsen/jgroups/workload/counter.clj:100-137). A counter
+// config's value is a function of its linearized set: every config at a RETURN step has
+// linearized the ops returned so far (base = the sum of their deltas) plus a subset m of the
+// pending slots, so value(m) = init + base + S(m), S(m) = the sum of m's deltas. The frontier is
+// therefore a bitmap over masks — one bit per config, no state bytes — and a step of op k from
+// mask m is consistent iff k is unconstrained (:add, :decr, a read of nil, a crashed
+// *-and-get) or S(m) equals k's requirement (a read of v: v - init - base; an :ok *-and-get
+// [d new]: new -/+ d - init - base).
+//
+// Layout: u64 word w covers the 64 masks (w << 6) | p; slots 0..5 are inside the word, slots
+// >= 6 index words. A RETURN is the subset DP over the popcount layers of the word index that
+// the register tables run (dense.hpp), with each op's consistency as a per-position gate:
+// S((w, p)) = S_hi(w) + S_lo(p), and the positions p of one word whose low sum equals a value
+// come from a 64-entry table EQ[v - lo_min] rebuilt per step.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace lc {
+
+constexpr int CTAB_LO = 6;          // slots inside a table word
+constexpr int CTAB_LMAX = 20;       // widest table a workgroup holds in LDS (2^20 bits = 128 KiB)
+constexpr int CTAB_MAX_NINV = 31;   // invocations per step (2 stream words each, a 128-word window;
+                                    // never binding: a step's invocations are live, <= CTAB_LMAX)
+constexpr int CTAB_DMAX = 10;       // |delta| of every op (EQ tables of 64 entries over 6 slots)
+constexpr int32_t CTAB_REQ_BIAS = 1 << 29;  // stream requirement bias (|req| < 2^29, else never)
+constexpr int64_t CTAB_SUM_MAX = 1 << 27;   // sum of |delta| over a history (bounds every config value)
+
+// Step stream (host-built, one u32 stream per history):
+//   header  live[0:24) | j[24:29), bit 31 clear (as dense.hpp)
+//   per invocation since the previous step, two words with bit 31 (DENSE_OPW) set:
+//     w0 = slot[0:8) | flags[8:16) | (uint8_t)delta[16:24)       flags: CT_UNC, CT_NEVER
+//     w1 = (req + CTAB_REQ_BIAS) & 0x3fffffff                   req: the value relative to the
+//          initial one the counter must hold before the op (when neither flag is set)
+constexpr uint32_t CT_UNC = 1u, CT_NEVER = 2u;
+
+struct CtabParams {
+  int32_t n;                     // histories in this launch (entries of order)
+  const int32_t* order;          // plan-local history ids, heaviest first
+  const int64_t* sbeg;           // [n_hist] first word of each history's stream
+  const int32_t* nsteps;         // [n_hist]
+  const int8_t* lmax;            // [n_hist] table width (bits)
+  const uint32_t* words;         // the sorted word list (dense_word_list, DENSE_WORD_BITS bits)
+  const uint32_t* stream;
+  int64_t stream_words;
+  int32_t* queue;                // dequeue counter (zeroed before launch)
+  int32_t* status;               // [n_hist] ST_VALID / ST_INVALID
+  int32_t* fail_step;            // [n_hist]
+  unsigned long long* explored;  // [n_hist]
+  unsigned long long* stats;     // [2] frontier configs out, steps
+  unsigned long long* stamps;    // [n_hist][2] start, end (s_memrealtime, 100 MHz); may be null
+  int32_t pipe;                  // bit 0: double-buffered tables when two fit (default on)
+};
+
+hipError_t launch_ctab(const CtabParams& p, int grid, hipStream_t stream);
+int ctab_grid_size();
+
+}  // namespace lc

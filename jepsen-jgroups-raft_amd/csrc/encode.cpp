@@ -402,15 +402,92 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
   o.inv_index.resize(keep);
 }
 
+std::vector<OneOut>& parts_of_thread() {
+  thread_local std::vector<OneOut> parts;
+  return parts;
+}
+
 }  // namespace
+
+void encode_trim() { std::vector<OneOut>().swap(parts_of_thread()); }
+
+void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out) {
+  const int n = (int)hs.size();
+  out.model = all.model;
+  out.n_hist = n;
+  out.init_value = all.init_value;
+  out.step_off.assign(n + 1, 0);
+  out.state_off.assign(n + 1, 0);
+  out.err.resize(n);
+  out.errmsg.resize(n);
+  out.live_max.resize(n);
+  out.n_states.resize(n);
+  out.n_ops.resize(n);
+  std::vector<int64_t> inv_base(n + 1, 0);
+  for (int i = 0; i < n; ++i) {
+    const int h = hs[i];
+    out.err[i] = all.err[h];
+    out.errmsg[i] = all.errmsg[h];
+    out.live_max[i] = all.live_max[h];
+    out.n_states[i] = all.n_states[h];
+    out.n_ops[i] = all.n_ops[h];
+    const int32_t g0 = all.step_off[h], g1 = all.step_off[h + 1];
+    out.step_off[i + 1] = out.step_off[i] + (g1 - g0);
+    out.state_off[i + 1] = out.state_off[i] + (all.state_off[h + 1] - all.state_off[h]);
+    inv_base[i + 1] = inv_base[i] + (all.inv_off[g1] - all.inv_off[g0]);
+  }
+  const int64_t ns = out.step_off[n], ni = inv_base[n];
+  out.state_val.resize(out.state_off[n]);
+  out.step_slot.resize(ns);
+  out.step_cmp_idx.resize(ns);
+  out.step_inv_idx.resize(ns);
+  out.inv_off.resize(ns + 1);
+  out.inv_off[0] = 0;
+  out.inv_slot.resize(ni);
+  out.inv_kind.resize(ni);
+  out.inv_a.resize(ni);
+  out.inv_b.resize(ni);
+  out.inv_index.resize(ni);
+  Pool::get().run(n, ns < 100000 ? 1 : 16, [&](int i) {
+    const int h = hs[i];
+    const int64_t g0 = all.step_off[h], m = all.step_off[h + 1] - g0, s0 = out.step_off[i];
+    std::copy_n(all.state_val.begin() + all.state_off[h], all.state_off[h + 1] - all.state_off[h],
+                out.state_val.begin() + out.state_off[i]);
+    std::copy_n(all.step_slot.begin() + g0, m, out.step_slot.begin() + s0);
+    std::copy_n(all.step_cmp_idx.begin() + g0, m, out.step_cmp_idx.begin() + s0);
+    std::copy_n(all.step_inv_idx.begin() + g0, m, out.step_inv_idx.begin() + s0);
+    const int64_t q0 = all.inv_off[g0], qn = all.inv_off[g0 + m] - q0, o0 = inv_base[i];
+    for (int64_t s = 0; s < m; ++s) out.inv_off[s0 + s + 1] = o0 + (all.inv_off[g0 + s + 1] - q0);
+    std::copy_n(all.inv_slot.begin() + q0, qn, out.inv_slot.begin() + o0);
+    std::copy_n(all.inv_kind.begin() + q0, qn, out.inv_kind.begin() + o0);
+    std::copy_n(all.inv_a.begin() + q0, qn, out.inv_a.begin() + o0);
+    std::copy_n(all.inv_b.begin() + q0, qn, out.inv_b.begin() + o0);
+    std::copy_n(all.inv_index.begin() + q0, qn, out.inv_index.begin() + o0);
+  });
+}
+
+void sink_encoded(const Encoded& enc, const HistSink& sink) {
+  const int64_t ns = enc.total_steps();
+  Pool::get().run(enc.n_hist, ns < 100000 ? 1 : 16, [&](int h) {
+    thread_local std::vector<int64_t> ninv;
+    const int64_t g0 = enc.step_off[h], m = enc.step_off[h + 1] - g0;
+    ninv.resize((size_t)m);
+    for (int64_t s = 0; s < m; ++s) ninv[s] = enc.inv_off[g0 + s + 1] - enc.inv_off[g0 + s];
+    const int64_t q0 = m > 0 ? enc.inv_off[g0] : 0;
+    sink(h, HistView{enc.err[h], enc.live_max[h], enc.n_states[h], enc.err[h] ? 0 : m, enc.step_slot.data() + g0,
+                     ninv.data(), enc.inv_slot.data() + q0, enc.inv_a.data() + q0, enc.inv_b.data() + q0,
+                     enc.inv_kind.data() + q0});
+  });
+}
 
 void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
             const HistArrays& a, Encoded& out, const HistSink* sink) {
   out.model = model;
   out.n_hist = n_hist;
   out.init_value = init_value;
-  // per-history parts, kept per calling thread across calls (their buffers keep capacity)
-  thread_local std::vector<OneOut> parts_tl;
+  // per-history parts, kept per calling thread across calls (their buffers keep capacity;
+  // encode_trim frees them)
+  std::vector<OneOut>& parts_tl = parts_of_thread();
   if ((int)parts_tl.size() < n_hist) parts_tl.resize(n_hist);
   for (int h = 0; h < n_hist; ++h) {
     OneOut& o = parts_tl[h];
@@ -432,7 +509,7 @@ void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
     if (sink)
       taken[h] = (*sink)(h, HistView{o.err, o.live_max, o.n_states, o.err ? 0 : (int64_t)o.step_slot.size(),
                                      o.step_slot.data(), o.step_ninv.data(), o.inv_slot.data(), o.inv_a.data(),
-                                     o.inv_b.data()});
+                                     o.inv_b.data(), o.inv_kind.data()});
   });
 
   // concatenate: offsets first, then every history's part copied in parallel

@@ -103,6 +103,7 @@ struct HistView {
   const uint8_t* inv_slot;
   const int64_t* inv_a;
   const int64_t* inv_b;
+  const uint8_t* inv_kind;  // counter / leader op kind bits (C_*)
 };
 // Called by the worker that encoded history h, right after it (its data still in cache).
 // Returns true when the caller has taken everything it needs of h's invocations: `out` then
@@ -115,5 +116,14 @@ using HistSink = std::function<bool(int, const HistView&)>;
 // every history as soon as it is encoded (lc_plan builds its dense step streams there).
 void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
             const HistArrays& a, Encoded& out, const HistSink* sink = nullptr);
+
+// The histories hs of `all` (encoded without a sink: every invocation array kept) as an Encoded
+// of their own, in that order: lc_check(n_gpus > 1) encodes a batch once and gives each shard
+// its histories this way (a parallel copy, no second encode).
+void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out);
+// sink(h, view) for every history of enc, the views built from enc's arrays (on the pool)
+void sink_encoded(const Encoded& enc, const HistSink& sink);
+// Frees the calling thread's encoder buffers (kept between calls for speed; lc_release).
+void encode_trim();
 
 }  // namespace lc

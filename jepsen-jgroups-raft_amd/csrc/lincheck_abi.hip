@@ -22,6 +22,7 @@
 
 #include "../../include/lincheck.h"
 #include "bounds.hpp"
+#include "ctab.hpp"
 #include "dense.hpp"
 #include "wide.hpp"
 #include "encode.hpp"
@@ -162,6 +163,12 @@ struct lc_plan {
   DevArray d_kscratch, d_kspill, d_kspillpos, d_kstatus, d_kfail, d_kexplored;
   // dense closure tables (narrow cas-register histories; dense.hpp)
   std::vector<int> dense_b, dense_w, dense_x, dense_m;  // block / wave / wide / mid teams, heaviest first
+  // counter histories on closure tables (ctab.hip), heaviest first
+  std::vector<int> dense_c;
+  int dgrid_c = 0;
+  int ctab_maxw = CTAB_LMAX;  // LC_CTAB_MAXW (0: counters take the grid kernel, tests)
+  int ctab_pipe = 1;          // LC_CTAB_PIPE: bit 0 double-buffered tables
+  DevArray d_cstats;
   DevArray d_dpack, d_dwords, d_dqueue, d_dstatus, d_dfail, d_dexpl;
   // histories wider than the LDS tile teams hold: tables in HBM (wide.hip)
   std::vector<int> dense_wd;
@@ -170,6 +177,7 @@ struct lc_plan {
   DevArray d_wtab, d_wstream, d_wmeta, d_wres, d_wbar;
   int wide_maxw = WIDE_LMAX, wide_minw = 0;  // LC_WIDE_MAXW (0: off) / LC_WIDE_MINW (tests)
   int wide_grid = 0;  // LC_WIDE_GRID: at most this many workgroups for the HBM tables (0: one per CU)
+  int wide_watchdog_ms = 20000;  // LC_WIDE_WATCHDOG_MS: a grid barrier's longest wait (tests force it low)
   bool wide_pipe = true;  // LC_WIDE_PIPE=0: one step at a time (a grid barrier per popcount layer)
   // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
   // begin / step count / table width, and the queue order
@@ -323,7 +331,7 @@ struct lc_plan {
     {
       // occupancy queries (hipGetDeviceProperties ~ms each) once per device and model; the
       // caller holds the device mutex
-      static struct { bool ok; int nwg, db, dw, dm, knwg; } cache[64][3];
+      static struct { bool ok; int nwg, db, dw, dm, knwg, dc; } cache[64][4];
       auto& c = cache[device & 63][model & 3];
       if (!c.ok) {
         // (LC_PHASES: the first query of a kernel loads the library's code object onto the
@@ -339,12 +347,13 @@ struct lc_plan {
         const double t_dense = ms_since(t1);
         t1 = std::chrono::steady_clock::now();
         c.knwg = keys_grid_size(model);
+        c.dc = ctab_grid_size();
         c.ok = c.nwg > 0 && c.knwg > 0;
         if (debug() || getenv("LC_PHASES"))
           fprintf(stderr, "[lincheck] first use of device %d: streams+events %.2f ms, occupancy queries: search %.2f "
                   "dense %.2f keys %.2f ms\n", device, t_ev, t_search, t_dense, ms_since(t1));
       }
-      nwg = c.nwg, dgrid_b = c.db, dgrid_w = c.dw, dgrid_m = c.dm, knwg = c.knwg;
+      nwg = c.nwg, dgrid_b = c.db, dgrid_w = c.dw, dgrid_m = c.dm, knwg = c.knwg, dgrid_c = c.dc;
     }
     if (nwg <= 0 || knwg <= 0) {
       last_error = "search kernels cannot be resident (occupancy 0)";
@@ -362,6 +371,9 @@ struct lc_plan {
     if ((e = getenv("LC_WIDE_MINW"))) wide_minw = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_PIPE"))) wide_pipe = atoi(e) != 0;
     if ((e = getenv("LC_WIDE_GRID"))) wide_grid = std::max(0, atoi(e));
+    if ((e = getenv("LC_WIDE_WATCHDOG_MS")) && atoi(e) >= 0) wide_watchdog_ms = atoi(e);
+    if ((e = getenv("LC_CTAB_MAXW"))) ctab_maxw = std::max(0, std::min(atoi(e), CTAB_LMAX));
+    if ((e = getenv("LC_CTAB_PIPE"))) ctab_pipe = atoi(e);
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e), pipe_env = true;
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
@@ -398,6 +410,7 @@ struct lc_plan {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
+    ctab_maxw = CTAB_LMAX, ctab_pipe = 1, wide_watchdog_ms = 20000;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.2, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 12, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, rot_chain_min = 14, batch_hist = 600, mid_maxw = 0;
@@ -526,7 +539,9 @@ struct lc_plan {
     dense_x.clear();
     dense_m.clear();
     dense_wd.clear();
-    dense_on = model == LC_MODEL_CAS_REGISTER && path == 0 && dgrid_b > 0 && dgrid_w > 0 && dgrid_m > 0;
+    dense_c.clear();
+    dense_on = (model == LC_MODEL_CAS_REGISTER && path == 0 && dgrid_b > 0 && dgrid_w > 0 && dgrid_m > 0) ||
+               (model == LC_MODEL_COUNTER && path == 0 && dgrid_c > 0 && ctab_maxw > 0);
     if (!dense_on) return 0;
     dense_ok.assign(n, 0);
     wide_ok.assign(n, 0);
@@ -539,7 +554,8 @@ struct lc_plan {
     // history h's range: its entry count + 1 words (every entry yields at most one word; the +1
     // holds the terminator the decoders need: a step's op words are counted up to the first word
     // without DENSE_OPW, which must not be a neighbour's stale word)
-    pack_words = hist_off[n] - hist_off[0] + n;
+    // (a counter step stream has two words per invocation: twice the entry count bounds it)
+    pack_words = (model == LC_MODEL_COUNTER ? 2 : 1) * (hist_off[n] - hist_off[0]) + n;
     // everything the dense kernels read goes up in ONE async copy from a pinned staging buffer
     // (kept across calls: no page faults, DMA at full rate): [words | sbeg | nsteps | order | lmax]
     o_sbeg = ((size_t)pack_words * 4 + 7) & ~(size_t)7;
@@ -555,13 +571,15 @@ struct lc_plan {
       hpack_bytes = pack_bytes + pack_bytes / 4;
     }
     int64_t* const sbeg = (int64_t*)(hpack + o_sbeg);
-    for (int h = 0; h < n; ++h) sbeg[h] = hist_off[h] - hist_off[0] + h;
+    const int64_t mul = model == LC_MODEL_COUNTER ? 2 : 1;
+    for (int h = 0; h < n; ++h) sbeg[h] = mul * (hist_off[h] - hist_off[0]) + h;
     return 0;
   }
   bool keep_inv_arrays = false;  // lc_failure_configs: its grid re-run needs every history's
   // returns true when h's step stream was built (its invocation arrays are then not needed)
   bool dense_sink(int h, const HistView& v) {
     if (!dense_on) return false;
+    if (model == LC_MODEL_COUNTER) return ctab_sink(h, v);
     int32_t* const nst = (int32_t*)(hpack + o_nst);
     int8_t* const lm = (int8_t*)(hpack + o_lm);
     dalg_tot[h] = StepBytes{0, 0};
@@ -641,6 +659,76 @@ struct lc_plan {
     wide_ok[h] = 1;
   }
 
+  // A counter history's step stream for the closure tables (ctab.hpp): each op as its delta and
+  // the value, relative to the initial one, the counter must hold before it (CounterModel.step,
+  // counter.clj:102-127: a read of v needs v; an :ok *-and-get [d new] needs new - d, or new + d
+  // for decr; both a pre- and a post-condition that disagree: never). Eligible: the table fits
+  // one workgroup's LDS (live width <= ctab_maxw), |delta| <= CTAB_DMAX, the deltas' absolute sum
+  // below CTAB_SUM_MAX (every config value then fits the kernel's int32 sums), at most
+  // CTAB_MAX_NINV invocations per step. The others take the grid kernel.
+  bool ctab_sink(int h, const HistView& v) {
+    int32_t* const nst = (int32_t*)(hpack + o_nst);
+    int8_t* const lm = (int8_t*)(hpack + o_lm);
+    nst[h] = 0;
+    lm[h] = 0;
+    dense_ok[h] = 0;
+    bool ok = !v.err && v.live_max <= ctab_maxw;
+    int64_t ni = 0;
+    for (int64_t t = 0; t < v.n_steps && ok; ++t) {
+      if (v.step_ninv[t] > CTAB_MAX_NINV) ok = false;
+      ni += v.step_ninv[t];
+    }
+    int64_t dsum = 0;
+    for (int64_t k = 0; k < ni && ok; ++k) {
+      const int64_t d = v.inv_b[k];
+      if ((v.inv_kind[k] & C_LEADER) || d > CTAB_DMAX || d < -CTAB_DMAX) ok = false;
+      dsum += d < 0 ? -d : d;
+    }
+    if (!ok || dsum >= CTAB_SUM_MAX) return false;
+    dense_ok[h] = 1;
+    nst[h] = (int32_t)v.n_steps;
+    lm[h] = (int8_t)std::max(1, v.live_max);
+    uint32_t* const out0 = (uint32_t*)hpack + ((const int64_t*)(hpack + o_sbeg))[h];
+    uint32_t* out = out0;
+    const int64_t init = enc.init_value;
+    uint32_t live = 0;
+    int64_t q = 0;
+    double cost = 0;
+    for (int64_t t = 0; t < v.n_steps; ++t) {
+      if (t > 0) live &= ~(1u << v.step_slot[t - 1]);
+      const int64_t q1 = q + v.step_ninv[t];
+      for (int64_t k = q; k < q1; ++k) live |= 1u << v.inv_slot[k];
+      *out++ = live | ((uint32_t)v.step_slot[t] << DENSE_J_SHIFT);
+      for (int64_t k = q; k < q1; ++k) {
+        const uint8_t kind = v.inv_kind[k];
+        const int64_t a = v.inv_a[k], delta = (kind & C_SUB) ? -v.inv_b[k] : v.inv_b[k];
+        uint32_t fl = 0;
+        int64_t req = 0;
+        if (!(kind & (C_PRE_EQ | C_POST_EQ))) {
+          fl = CT_UNC;
+        } else {
+          int64_t r_pre = 0, r_post = 0;
+          bool never = false;
+          if (kind & C_PRE_EQ) never |= __builtin_sub_overflow(a, init, &r_pre);
+          if (kind & C_POST_EQ) never |= __builtin_sub_overflow(a, init, &r_post) || __builtin_sub_overflow(r_post, delta, &r_post);
+          req = (kind & C_PRE_EQ) ? r_pre : r_post;
+          if ((kind & C_PRE_EQ) && (kind & C_POST_EQ) && r_pre != r_post) never = true;
+          if (req >= CTAB_REQ_BIAS || req < -CTAB_REQ_BIAS) never = true;  // no config reaches it
+          if (never) fl = CT_NEVER, req = 0;
+        }
+        *out++ = (uint32_t)v.inv_slot[k] | (fl << 8) | ((uint32_t)(uint8_t)(int8_t)delta << 16) | DENSE_OPW;
+        *out++ = ((uint32_t)(req + CTAB_REQ_BIAS) & 0x3fffffffu) | DENSE_OPW;
+      }
+      const int L = live ? 32 - __builtin_clz(live) : 0;
+      cost += std::ldexp(1.0, std::max(0, L - CTAB_LO)) + 8.0;
+      q = q1;
+    }
+    dense_cost[h] = cost;
+    dense_nw[h] = out - out0;
+    *out = 0u;  // the terminator (no DENSE_OPW)
+    return !keep_inv_arrays;
+  }
+
   int build_dense() {
     const auto t_build = std::chrono::steady_clock::now();
     auto ms_since_build = [&] {
@@ -659,6 +747,10 @@ struct lc_plan {
       if (wide_ok[h]) dense_wd.push_back(h);
     for (int h = 0; h < n; ++h) {
       if (!ok[h]) continue;
+      if (model == LC_MODEL_COUNTER) {
+        dense_c.push_back(h);
+        continue;
+      }
       const int lw = enc.live_max[h];
       // MID teams (several per CU) take the narrower BLOCK histories when BLOCK steps are pipelined
       (lw <= DENSE_WAVE_LMAX ? dense_w
@@ -720,9 +812,10 @@ struct lc_plan {
     std::stable_sort(dense_w.begin(), dense_w.end(), heavy_first);
     std::stable_sort(dense_x.begin(), dense_x.end(), heavy_first);
     std::stable_sort(dense_m.begin(), dense_m.end(), heavy_first);
+    std::stable_sort(dense_c.begin(), dense_c.end(), heavy_first);
     {
       int32_t* o = ordp;
-      for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
+      for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m, &dense_c})
         o = std::copy(ids->begin(), ids->end(), o);
     }
     dstream_words = pack_words;
@@ -1575,6 +1668,92 @@ struct lc_plan {
     return free_b;
   }
 
+  // Counter histories on closure tables (ctab.hip): one launch, one history per 1024-thread
+  // workgroup (dequeued heaviest first), their step streams already in d_dpack.
+  int run_ctab(float* ms) {
+    const int nc = (int)dense_c.size();
+    if (!nc) return 0;
+    const int n = enc.n_hist;
+    HIP_TRY(d_cstats.ensure(16));
+    ZeroSpans z;
+    z.add((char*)d_dqueue.p + 12, 4);
+    z.add(d_cstats.p, 16);
+    z.add(d_dexpl.p, (size_t)std::max(n, 1) * 8);
+    HIP_TRY(zero_spans(z, stream));
+    CtabParams p{};
+    p.n = nc;
+    p.order = dp_ord + (dense_b.size() + dense_w.size() + dense_x.size() + dense_m.size());
+    p.sbeg = dp_sbeg;
+    p.nsteps = dp_nst;
+    p.lmax = dp_lm;
+    p.words = d_dwords.as<uint32_t>();
+    p.stream = dp_stream;
+    p.stream_words = dstream_words;
+    p.queue = (int32_t*)((char*)d_dqueue.p + 12);
+    p.status = d_dstatus.as<int32_t>();
+    p.fail_step = d_dfail.as<int32_t>();
+    p.explored = d_dexpl.as<unsigned long long>();
+    p.stats = d_cstats.as<unsigned long long>();
+    p.pipe = ctab_pipe;
+    if (debug()) {
+      HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
+      HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
+      p.stamps = d_dstamps.as<unsigned long long>();
+    }
+    const int grid = std::min(nc, dgrid_c);
+    HIP_TRY(hipEventRecord(ev0, stream));
+    HIP_TRY(launch_ctab(p, grid, stream));
+    HIP_TRY(hipEventRecord(ev1, stream));
+    const size_t need = (size_t)n * 16 + 16;
+    if (hstage_bytes < need) {
+      if (hstage) HIP_TRY(hipHostFree(hstage));
+      hstage = nullptr;
+      HIP_TRY(hipHostMalloc(&hstage, need, hipHostMallocDefault));
+      hstage_bytes = need;
+    }
+    unsigned long long* const ex = hstage;
+    int32_t* const st = reinterpret_cast<int32_t*>(hstage + n);
+    int32_t* const fs = st + n;
+    unsigned long long* const cs = reinterpret_cast<unsigned long long*>(fs + n);
+    HIP_TRY(hipMemcpyAsync(ex, d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(st, d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(fs, d_dfail.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(cs, d_cstats.p, 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
+    *ms += t;
+    double expl = 0;
+    for (int h : dense_c) {
+      status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
+      expl += (double)ex[h];
+    }
+    stats[1] += 1;
+    stats[2] += (double)cs[1];
+    stats[4] += (double)cs[0] + nc;  // frontier in = previous frontier out (+ the initial config)
+    stats[6] += (double)cs[0];
+    stats[12] += nc;
+    stats[13] += t;
+    stats[34] += nc;
+    stats[35] += t;
+    stats[36] += (double)cs[0] + nc;
+    stats[37] += (double)cs[0];
+    stats[38] += expl;
+    if (debug()) {
+      fprintf(stderr, "[lincheck] ctab: %d counter histories on %d workgroups: %.3f ms, steps=%llu Fout=%llu\n", nc,
+              grid, t, cs[1], cs[0]);
+      std::vector<unsigned long long> T((size_t)n * 4);
+      if (hipMemcpy(T.data(), d_dstamps.p, (size_t)n * 16, hipMemcpyDeviceToHost) == hipSuccess)
+        for (int i = 0; i < nc && i < 4; ++i) {
+          const int h = dense_c[i];
+          fprintf(stderr, "[lincheck]   h=%d width=%d steps=%d: %.1f us (%.3f us/step)\n", h, enc.live_max[h],
+                  enc.n_steps(h), (T[2 * h + 1] - T[2 * h]) / 100.0,
+                  (T[2 * h + 1] - T[2 * h]) / 100.0 / std::max(1, enc.n_steps(h)));
+        }
+    }
+    return 0;
+  }
+
   // The wide histories (tables in HBM), one persistent launch over the whole GPU, one history
   // after another. `ran` stays false when the two tables do not fit the device (they then take
   // the grid kernel, as before).
@@ -1642,6 +1821,7 @@ struct lc_plan {
     p.anyv = (uint32_t*)(p.stats + 2);
     p.bar = d_wbar.as<unsigned>();
     p.abort = (int32_t*)((char*)d_wbar.p + wide_bar_bytes());
+    p.watchdog = (uint64_t)wide_watchdog_ms * 100000ull;
     const int grid = wide_grid > 0 ? std::min(wide_grid, wide_grid_size()) : wide_grid_size();
     if (grid < 1) {
       last_error = "wide kernel: no resident workgroups";
@@ -1658,17 +1838,19 @@ struct lc_plan {
     float t = 0;
     HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
     *ms += t;
-    if (ab) {
-      last_error = "wide kernel: grid barrier watchdog fired";
-      return LC_E_INTERNAL;
-    }
     const int32_t* st = (const int32_t*)(res.data() + 2 * nwd);
     const int32_t* fs = st + nwd;
     const unsigned long long* ss = (const unsigned long long*)(fs + nwd);
+    // a watchdog abort (a grid barrier stalled: the cooperative grid assumes the whole
+    // device, so another user of it can starve a workgroup) leaves the histories it had not
+    // finished undecided (LC_H_ABORTED, :unknown); the finished ones and the rest of the call
+    // keep their answers
     for (int i = 0; i < nwd; ++i) {
       const int h = dense_wd[i];
-      status[h] = st[i], fail_step[h] = fs[i], explored[h] = res[i];
+      const bool unfinished = st[i] != ST_VALID && st[i] != ST_INVALID;
+      status[h] = ab && unfinished ? ST_ABORTED : st[i], fail_step[h] = fs[i], explored[h] = res[i];
     }
+    if (ab && debug()) fprintf(stderr, "[lincheck] wide: grid barrier watchdog fired after %.1f ms\n", t);
     stats[1] += 1;
     stats[2] += (double)ss[1];
     stats[12] += nwd;  // (dense histories: LDS or HBM tables)
@@ -1758,6 +1940,10 @@ struct lc_plan {
       for (int h : dense_x) done[h] = 1;
       for (int h : dense_m) done[h] = 1;
     }
+    if (max_t == INT32_MAX && path == 0 && dense_on && !dense_c.empty()) {
+      if ((rc = run_ctab(&ms))) return rc;
+      for (int h : dense_c) done[h] = 1;
+    }
     if (max_t == INT32_MAX && path == 0 && dense_on && !dense_wd.empty()) {
       bool ran = false;
       if ((rc = run_wide(&ms, ran))) return rc;
@@ -1807,6 +1993,7 @@ struct lc_plan {
           break;
         }
         case ST_CAPACITY: code = LC_H_CAPACITY; break;
+        case ST_ABORTED: code = LC_H_ABORTED; break;
         case ST_MODEL: code = LC_H_MODEL; break;
         default: break;
       }
@@ -1824,9 +2011,13 @@ namespace {
 
 // Encode histories and upload them into plan `reuse` (its device buffers, streams and events
 // kept: lc_check's per-device cached plan) or into a new plan.
+// `pre` (lc_check with n_gpus > 1): the whole batch already encoded once; this plan takes its
+// histories `pre_hs` (hist_off = their entry offsets) by copying their encoded arrays
+// (encoded_subset) and builds its dense step streams from them, with no second encode.
 int plan_build(int device, int model, int64_t init_value, int n_hist, const int64_t* hist_off,
                const HistArrays& a, int64_t max_configs, lc_plan** out, std::string& msg,
-               lc_plan* reuse = nullptr, bool keep_inv_arrays = false) {
+               lc_plan* reuse = nullptr, bool keep_inv_arrays = false, const Encoded* pre = nullptr,
+               const std::vector<int>* pre_hs = nullptr) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) {
     return std::chrono::duration<double, std::milli>(clk::now() - t).count();
@@ -1844,7 +2035,10 @@ int plan_build(int device, int model, int64_t init_value, int n_hist, const int6
   auto t = clk::now();
   // the dense step streams are written by the encoder's workers as each history is encoded
   if (!rc) rc = p->dense_prepare(n_hist, hist_off);
-  if (!rc) {
+  if (!rc && pre) {
+    encoded_subset(*pre, *pre_hs, p->enc);
+    if (p->dense_on) sink_encoded(p->enc, [p](int h, const HistView& v) { return p->dense_sink(h, v); });
+  } else if (!rc) {
     const HistSink sink = [p](int h, const HistView& v) { return p->dense_sink(h, v); };
     encode(model, init_value, n_hist, hist_off, a, p->enc, p->dense_on ? &sink : nullptr);
   }
@@ -1926,15 +2120,13 @@ void lpt_shards(int n_hist, const int64_t* off, int G, int32_t* out_shard) {
 // 55 us per step at width 27, 190 at width 30 on the crash ramp). Counter histories and
 // histories no table takes (the grid kernel) cost their entry count (one unit per entry). Host
 // only.
-void history_costs(int model, int64_t init_value, int n_hist, const int64_t* off, const HistArrays& a,
-                   std::vector<double>& cost) {
+void history_costs_of(const Encoded& enc, const int64_t* off, std::vector<double>& cost) {
+  const int n_hist = enc.n_hist;
   cost.assign(n_hist, 0.0);
-  if (model != LC_MODEL_CAS_REGISTER) {
+  if (enc.model != LC_MODEL_CAS_REGISTER) {
     for (int h = 0; h < n_hist; ++h) cost[h] = (double)(off[h + 1] - off[h]);
     return;
   }
-  Encoded enc;
-  encode(model, init_value, n_hist, off, a, enc);
   for (int h = 0; h < n_hist; ++h) {
     const int lw = enc.live_max[h];
     if (enc.err[h] || enc.n_states[h] > DENSE_MAX_STATES || lw > WIDE_LMAX) {
@@ -1965,6 +2157,13 @@ void history_costs(int model, int64_t init_value, int n_hist, const int64_t* off
     }
     cost[h] = t;
   }
+}
+void history_costs(int model, int64_t init_value, int n_hist, const int64_t* off, const HistArrays& a,
+                   std::vector<double>& cost) {
+  Encoded enc;
+  if (model == LC_MODEL_CAS_REGISTER) encode(model, init_value, n_hist, off, a, enc);
+  else enc.model = model, enc.n_hist = n_hist;
+  history_costs_of(enc, off, cost);
 }
 
 // LPT over G shards by cost: heaviest first, each to the least-loaded shard (lowest index on
@@ -2110,12 +2309,23 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
   // shard histories over devices: longest-processing-time on each history's modeled chain time
   // (lc_shard_histories_by_cost; a shard lasts as long as its slowest chains)
   std::vector<std::vector<int>> shard(G);
+  // n_gpus > 1: the batch is encoded ONCE (its modeled costs split it; each shard's plan then
+  // copies its histories' encoded arrays instead of gathering and re-encoding the raw ones)
+  Encoded all;
   if (G > 1) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    encode(model_kind, init_value, n_hist, off0.data(), HistArrays{off0[n_hist], cidx, cpr, cty, cf, cv0, cv1, cvf},
+           all);
+    const auto t1 = clk::now();
     std::vector<int32_t> of(n_hist);
     std::vector<double> cost;
-    history_costs(model_kind, init_value, n_hist, off0.data(),
-                  HistArrays{off0[n_hist], cidx, cpr, cty, cf, cv0, cv1, cvf}, cost);
+    history_costs_of(all, off0.data(), cost);
     lpt_by_cost(n_hist, cost, G, of.data());
+    if (debug() || getenv("LC_PHASES"))
+      fprintf(stderr, "[lincheck] lc_check(n_gpus=%d): one encode %.2f ms, cost split %.2f ms\n", G,
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(clk::now() - t1).count());
     for (int h = 0; h < n_hist; ++h) shard[of[h]].push_back(h);
   } else {
     for (int h = 0; h < n_hist; ++h) shard[0].push_back(h);
@@ -2126,40 +2336,20 @@ int32_t lc_check(int32_t model_kind, int64_t init_value, int32_t n_hist, const i
   auto work = [&](int g) {
     const std::vector<int>& hs = shard[g];
     if (hs.empty()) return;
-    // this shard's histories as contiguous arrays: the caller's, in place, for one shard;
-    // else gathered (each history a contiguous run)
-    std::vector<int64_t> off(1, 0), idx, a0, a1;
-    std::vector<int32_t> pr;
-    std::vector<int8_t> ty, ff, vf;
-    HistArrays a{off0[n_hist], cidx, cpr, cty, cf, cv0, cv1, cvf};
+    // one shard: the caller's arrays in place; several: this shard's histories of the batch
+    // encoded once above (only their entry offsets here, for the dense streams' layout)
+    std::vector<int64_t> off(1, 0);
+    const HistArrays a{off0[n_hist], cidx, cpr, cty, cf, cv0, cv1, cvf};
     const int64_t* offp = off0.data();
     if (G > 1) {
-      int64_t n = 0;
-      for (int h : hs) n += off0[h + 1] - off0[h];
-      if (cidx) idx.resize(n);
-      pr.resize(n), ty.resize(n), ff.resize(n), a0.resize(n), a1.resize(n), vf.resize(n);
-      int64_t o = 0;
-      for (int h : hs) {
-        const int64_t b = off0[h], m = off0[h + 1] - b;
-        if (cidx) std::copy_n(cidx + b, m, idx.data() + o);
-        std::copy_n(cpr + b, m, pr.data() + o);
-        std::copy_n(cty + b, m, ty.data() + o);
-        std::copy_n(cf + b, m, ff.data() + o);
-        std::copy_n(cv0 + b, m, a0.data() + o);
-        std::copy_n(cv1 + b, m, a1.data() + o);
-        std::copy_n(cvf + b, m, vf.data() + o);
-        o += m;
-        off.push_back(o);
-      }
-      a = HistArrays{n, cidx ? idx.data() : nullptr, pr.data(), ty.data(), ff.data(), a0.data(), a1.data(),
-                     vf.data()};
+      for (int h : hs) off.push_back(off.back() + off0[h + 1] - off0[h]);
       offp = off.data();
     }
     const int dev = g % ndev;
     std::lock_guard<std::mutex> lk(device_mutex(dev));
     lc_plan* p = nullptr;
     int rc = plan_build(dev, model_kind, init_value, (int)hs.size(), offp, a, max_configs, &p, msgs[g],
-                        cached_plan(dev));
+                        cached_plan(dev), false, G > 1 ? &all : nullptr, &hs);
     if (!rc) {
       rc = p->run();
       if (rc) msgs[g] = p->last_error;
@@ -2232,6 +2422,8 @@ int32_t lc_release(int32_t device) {
     delete c;
     c = nullptr;
   }
+  // the calling thread's encoder buffers (kept between calls) go too
+  encode_trim();
   return 0;
 }
 

@@ -16,7 +16,7 @@ constexpr uint64_t EMPTY = ~0ull;
 constexpr uint64_t MARK = 1ull << 63; // "returned directly" routing marker
 
 enum : int32_t { ST_RUNNING = 0, ST_VALID = 1, ST_INVALID = 2, ST_CAPACITY = 3, ST_MODEL = 4,
-                 ST_SKIP = 5 };
+                 ST_SKIP = 5, ST_ABORTED = 6 };
 enum : int32_t { FL_ABORT = 0, FL_OVERFLOW = 1, FL_SPILL = 2, FL_N = 4 };
 enum : int32_t { SS_FIN = 0, SS_CAND = 1, SS_FOUT = 2, SS_SNEW = 3, SS_SPILL = 4, SS_PHASES = 5,
                  SS_STEPS = 6, SS_N = 8 };

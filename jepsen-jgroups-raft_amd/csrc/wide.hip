@@ -41,8 +41,8 @@ struct WideBar {  // two-level arrival counters + generation, each on its own 12
 
 // Grid barrier (search.hip's grid_sync without fences): every wave drains its sc1 stores, one
 // lane per workgroup arrives on its group's counter, the last of a group on the top counter,
-// the last of those bumps the generation the others poll (relaxed loads, s_sleep); 20 s
-// without a release raises *abort. The table words are sc1 stores read with sc1 loads.
+// the last of those bumps the generation the others poll (relaxed loads, s_sleep); p.watchdog
+// (20 s by default) without a release raises *abort. The table words are sc1 stores read with sc1 loads.
 __device__ __forceinline__ bool wide_sync(const WideParams& p, int* sAbort) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -65,7 +65,7 @@ __device__ __forceinline__ bool wide_sync(const WideParams& p, int* sAbort) {
     while (ld_agent(&bar->gen) == g) {
       __builtin_amdgcn_s_sleep(1);
       if ((++spins & 255) == 0) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > p.watchdog) {
           st_agent(p.abort, 1);
           break;
         }

@@ -41,6 +41,7 @@ struct WideParams {
   unsigned long long* stats;  // [2] frontier-out configs, steps
   int32_t pipe;               // 1: pipelined steps (wide_pipe_kernel), 0: one step at a time
   uint32_t* anyv;             // pipelined: per history, bit t = some X of step t was nonzero (zeroed)
+  uint64_t watchdog;          // s_memrealtime ticks (100 MHz) a grid barrier may wait before *abort
   const int64_t* anyv_off;    // [n] word offset of each history's bits (ns / 32 + 1 words)
 };
 

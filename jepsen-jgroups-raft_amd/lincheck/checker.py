@@ -21,7 +21,8 @@ from .model import Inconsistent, Model, step
 
 VALID = {1: True, 0: False, 2: "unknown"}
 ERRORS = {0: None, -4: "malformed history", -5: "too many concurrently pending ops",
-          -6: "model cannot step an op", -7: "frontier exceeded max-configs / device capacity"}
+          -6: "model cannot step an op", -7: "frontier exceeded max-configs / device capacity",
+          -8: "device search aborted by its barrier watchdog (device not wholly available)"}
 
 
 def merge_valid(vs: Sequence[Any]):

@@ -158,11 +158,21 @@ def gen_register(n_ops: int, n_clients: int, p_info: float, seed: int,
 
 
 def gen_counter(n_ops: int, n_clients: int, p_info: float, seed: int,
-                invalid: bool = False) -> History:
+                invalid: bool = False, n_crashed: int | None = None,
+                crash_span: float = 1.0) -> History:
+    """n_crashed: exactly that many non-read ops time out (:info), drawn uniformly from the first
+    `crash_span` of the ops (SURVEY §8(d) C5's exact-search variant, "<= ~15 crashed total");
+    p_info then only makes reads :fail. Default (None): every non-read op crashes with
+    probability p_info (the bounds-scan workload)."""
     rng = np.random.default_rng(seed)
     fs = np.array([F_READ, F_ADD, F_DECR, F_AAG, F_DAG], np.int8)[rng.integers(0, 5, n_ops)]
     d = rng.integers(0, 5, n_ops)
-    client, inv, cmp_, lin, crashed, read_fail, app_c = _schedule(rng, n_ops, n_clients, p_info, fs)
+    crash_idx = None
+    if n_crashed is not None:
+        span = np.nonzero(fs[:max(1, int(n_ops * crash_span))] != F_READ)[0]
+        crash_idx = np.random.default_rng(seed ^ 0xC5A5).choice(span, min(n_crashed, len(span)), replace=False)
+    client, inv, cmp_, lin, crashed, read_fail, app_c = _schedule(rng, n_ops, n_clients, p_info, fs,
+                                                                  crash_idx)
     typ = np.full(n_ops, T_OK, np.int8)
     res = np.zeros(n_ops, np.int64)
     state = 0
@@ -254,16 +264,24 @@ CONFIGS = {
     "c3": dict(kind="register", n_keys=1000, ops=1000, clients=5, p_info=0.01),
     "c4": dict(kind="register", n_keys=1, ops=100000, clients=16, p_info=1.5e-4),
     "c5": dict(kind="counter", n_keys=1, ops=1000000, clients=16, p_info=0.01),
+    # counter histories for the exact search: c2c is C2's shape as a counter
+    # (1 key x 5k ops, 16 clients, no crashes); c5x is C5's low-crash exact-search variant (SURVEY
+    # §8(d): "exact search: <= ~15 crashed total"): 4 crashed ops in the first 1 % of the history,
+    # so they stay pending (live) through all 1M ops; p_info 0.01 only fails reads
+    "c2c": dict(kind="counter", n_keys=1, ops=5000, clients=16, p_info=0.0, seed=12345),
+    "c5x": dict(kind="counter", n_keys=1, ops=1000000, clients=16, p_info=0.01, n_crashed=4,
+                crash_span=0.01),
 }
 
 
 def gen_config(name: str, key0: int = 0, scale: float = 1.0) -> History:
     c = CONFIGS[name]
-    cid = int(name[1:])
+    cid = int(name[1])
     ops = max(1, int(c["ops"] * scale)) if c["n_keys"] == 1 else c["ops"]
     n_keys = c["n_keys"] if c["n_keys"] == 1 else max(1, int(c["n_keys"] * scale))
     if c["kind"] == "counter":
-        h = gen_counter(ops, c["clients"], c["p_info"], seed_for(cid, key0))
+        h = gen_counter(ops, c["clients"], c["p_info"], c.get("seed", seed_for(cid, key0)),
+                        n_crashed=c.get("n_crashed"), crash_span=c.get("crash_span", 1.0))
         h.keys = [key0]
         return h
     return gen_register_keys(n_keys, ops, c["clients"], c["p_info"], config_id=cid, key0=key0)

@@ -1127,6 +1127,28 @@ def test_gpu_wide_tables_past_the_tile_teams():
     assert int(g["valid"][0]) == 1 and int(g["explored"][0]) > 0
 
 
+def test_gpu_wide_watchdog_abort_is_unknown(monkeypatch):
+    """when the HBM tables' grid barrier watchdog fires (forced here with
+    LC_WIDE_WATCHDOG_MS=0) the call still succeeds: the wide histories it did not finish are
+    :unknown with LC_H_ABORTED, every other history of the call keeps its answer."""
+    monkeypatch.setenv("LC_WIDE_MINW", "12")
+    monkeypatch.setenv("LC_WIDE_WATCHDOG_MS", "0")
+    narrow = [synth.gen_register(200, 4, 0.01, 56000 + t, invalid=(t % 2 == 1)) for t in range(6)]
+    wide = synth.gen_register(400, 16, 0.01, 56100, n_crashed=2)
+    h = H.concat(narrow + [wide])
+    assert _live_width(h, h.n_hist - 1) >= 12 and all(_live_width(h, k) < 12 for k in range(len(narrow)))
+    g = _lib.check(1, 0, h)
+    assert _lib.check_stats()["wide_histories"] == 1
+    last = h.n_hist - 1
+    assert int(g["valid"][last]) == 2 and int(g["err"][last]) == -8
+    exp = oracle.check_many("cas-register", h.select(list(range(len(narrow)))))
+    for k in range(len(narrow)):
+        _cmp(g, exp[k], k, "beside an aborted wide history")
+    monkeypatch.delenv("LC_WIDE_WATCHDOG_MS")
+    g2 = _lib.check(1, 0, h)  # the next call runs normally
+    assert int(g2["valid"][last]) == oracle.check_one("cas-register", h.select([last]))["valid"]
+
+
 def test_gpu_fuzz_register_and_counter_vs_oracle():
     """Random histories of both models, one lc_check per model (the batch planner sees them all
     together): 1-8 clients, 1-400 ops, 0-4 crashed writes/cas, :info on any op, valid and

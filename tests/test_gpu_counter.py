@@ -1,0 +1,176 @@
+"""GPU parity tests of the counter workload's exact search: the counter
+closure tables (csrc/ctab.hip) through the C-ABI against the CPU oracle and the
+oracle-pinned fixtures of tests/golden/counter_*_oracle.json (tests/golden/pin_counter.py).
+
+The reference checks a counter run as ONE whole-history knossos.linear search with CounterModel
+(src/jepsen/jgroups/workload/counter.clj:100-137); these tests hold the GPU's answer for that
+search — verdict, failing :index triple and explored count — to the oracle's at C2's shape
+(1 key x 5k ops, 16 clients), with crashed ops, and at C5's low-crash exact-search size."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from lincheck import _lib, history as H, synth
+
+pytestmark = pytest.mark.gpu
+GOLD_DIR = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if _lib.load().lc_device_count() < 1:
+        pytest.fail("no HIP device on a GPU run: the checker has no CPU fallback")
+
+
+def _cmp(got, exp, k=0, what=""):
+    assert int(got["valid"][k]) == exp["valid"], (what, k, got["valid"][k], exp)
+    assert int(got["fail_idx"][k]) == exp["fail_idx"], (what, k, got["fail_idx"][k], exp)
+    assert int(got["fail_inv"][k]) == exp["fail_inv_idx"], (what, k)
+    assert int(got["prev_ok"][k]) == exp["prev_ok_idx"], (what, k)
+    if exp["valid"] != 2:
+        assert int(got["explored"][k]) == exp["explored"], (what, k, got["explored"][k], exp)
+
+
+def _fixture(name):
+    p = os.path.join(GOLD_DIR, f"counter_{name}_oracle.json")
+    if not os.path.exists(p):
+        pytest.skip(f"{p} not pinned yet (tests/golden/pin_counter.py {name})")
+    return json.load(open(p))
+
+
+def _ctab_count():
+    return int(_lib.check_stats(0)["ctab_histories"])
+
+
+def _mixed_counters(n, seed0, max_ops=300, max_clients=16, max_crash=3):
+    rng = random.Random(seed0)
+    hs = []
+    for t in range(n):
+        k = rng.randint(0, max_crash)
+        hs.append(synth.gen_counter(rng.randint(1, max_ops), rng.randint(1, max_clients),
+                                    rng.choice([0.0, 0.02, 0.1]), seed0 * 1000 + t,
+                                    invalid=(t % 3 == 2), n_crashed=k if k else None))
+    return H.concat(hs)
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_gpu_ctab_random_vs_oracle(pipe, monkeypatch):
+    """Many counter histories in one lc_check (one per workgroup, dequeued heaviest first):
+    1-16 clients, crashed ops, :fail reads, perturbed reads; double-buffered tables and the
+    single-table form (LC_CTAB_PIPE=0, a step two super-layers after its predecessor)."""
+    monkeypatch.setenv("LC_CTAB_PIPE", pipe)
+    h = _mixed_counters(240, 31)
+    g = _lib.check(2, 0, h)
+    assert _ctab_count() == h.n_hist
+    exp = oracle.check_many("counter", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"ctab pipe={pipe}")
+    assert any(e["valid"] == 0 for e in exp) and any(e["valid"] == 1 for e in exp)
+
+
+def test_gpu_ctab_matches_grid_kernel(monkeypatch):
+    """The same batch on the closure tables and on the grid kernel (LC_CTAB_MAXW=0)."""
+    h = _mixed_counters(60, 47, max_ops=200)
+    a = _lib.check(2, 0, h)
+    assert _ctab_count() == h.n_hist
+    monkeypatch.setenv("LC_CTAB_MAXW", "0")
+    b = _lib.check(2, 0, h)
+    assert _ctab_count() == 0
+    for key in ("valid", "fail_idx", "fail_inv", "prev_ok", "explored", "err"):
+        assert np.array_equal(a[key], b[key]), key
+
+
+@pytest.mark.parametrize("init", [0, 7, -123456, 2**40])
+def test_gpu_ctab_init_value(init):
+    """Requirements are relative to the initial value (counter.clj:133: (CounterModel. 0); the
+    C-ABI takes any init_value)."""
+    hs = [synth.gen_counter(150, 8, 0.02, 5100 + t, invalid=(t % 2 == 1)) for t in range(6)]
+    h = H.concat(hs)
+    g = _lib.check(2, init, h)
+    for k in range(h.n_hist):
+        _cmp(g, oracle.check_one("counter", h.select([k]), init_value=init), k, f"init={init}")
+
+
+def test_gpu_ctab_wide_deltas_and_widths_route_to_grid():
+    """Histories the tables do not take (|delta| > 10, wider than 20 live slots) go to the grid
+    kernel in the same call; every answer still matches the oracle."""
+    big = synth.gen_counter(120, 5, 0.0, 77)
+    big.v0 = np.where((big.f == 3) & (big.vflags == 1), big.v0 * 20, big.v0)  # adds of 0..80
+    big = H.from_columns(big.index, big.process, big.type, big.f, big.v0, big.v1, big.vflags)
+    wide = synth.gen_counter(160, 16, 0.0, 78, n_crashed=6, crash_span=0.1)
+    ok = synth.gen_counter(200, 8, 0.0, 79)
+    h = H.concat([big, wide, ok])
+    g = _lib.check(2, 0, h)
+    exp = oracle.check_many("counter", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, "routing")
+    assert _ctab_count() >= 1
+
+
+def test_gpu_ctab_edge_histories():
+    """Empty, invoke-only, one op, a read of nil, decr-and-get and a *-and-get that crashed."""
+    E = lambda *ev: H.encode([dict(zip(("process", "type", "f", "value"), e)) for e in ev])  # noqa: E731
+    cases = [
+        E(),
+        E((0, "invoke", "add", 3)),
+        E((0, "invoke", "add", 3), (0, "ok", "add", 3)),
+        E((0, "invoke", "read", None), (0, "ok", "read", None)),
+        E((0, "invoke", "decr-and-get", 2), (0, "ok", "decr-and-get", [2, -2]),
+          (1, "invoke", "read", None), (1, "ok", "read", -2)),
+        E((0, "invoke", "add-and-get", 4), (0, "info", "add-and-get", 4),
+          (1, "invoke", "read", None), (1, "ok", "read", 4)),
+        E((0, "invoke", "add-and-get", 4), (0, "info", "add-and-get", 4),
+          (1, "invoke", "read", None), (1, "ok", "read", 3)),
+        E((0, "invoke", "add", 1), (1, "invoke", "read", None), (1, "ok", "read", 2), (0, "ok", "add", 1)),
+    ]
+    h = H.concat(cases)
+    g = _lib.check(2, 0, h)
+    exp = oracle.check_many("counter", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"edge {k}")
+
+
+def test_gpu_ctab_c2c_full_size_vs_fixture():
+    """C2's shape as a counter (1 key x 5k ops, 16 clients) at full size, against the oracle's
+    pinned answer (tests/golden/counter_c2c_oracle.json)."""
+    fx = _fixture("c2c")
+    h = synth.gen_config("c2c")
+    assert h.n == fx["n_entries"] and h.n_ops() == fx["n_ops"]
+    g = _lib.check(2, 0, h)
+    assert _ctab_count() == 1
+    assert int(g["valid"][0]) == fx["valid"] and int(g["fail_idx"][0]) == fx["fail_idx"]
+    assert int(g["explored"][0]) == fx["explored"]
+
+
+def test_gpu_ctab_c2c_crashed_vs_fixture():
+    """The same shape with 4 crashed ops pending through the rest of the history (width 20)."""
+    fx = _fixture("c2c4")
+    h = synth.gen_counter(5000, 16, 0.0, 12345, n_crashed=4)
+    assert h.n == fx["n_entries"]
+    g = _lib.check(2, 0, h)
+    assert _ctab_count() == 1
+    assert int(g["valid"][0]) == fx["valid"] and int(g["explored"][0]) == fx["explored"]
+
+
+def test_gpu_ctab_c2c_perturbed_prefixes_vs_oracle():
+    """C2c perturbed at random reads (invalid): the failing :index triple and explored count of
+    every prefix the oracle finishes quickly."""
+    for seed in range(3):
+        h = synth.gen_counter(2500, 16, 0.0, 6100 + seed, invalid=True)
+        g = _lib.check(2, 0, h)
+        _cmp(g, oracle.check_one("counter", h), 0, f"c2c-invalid-{seed}")
+
+
+def test_gpu_ctab_c5x_full_size_vs_fixture():
+    """C5's low-crash exact-search variant (1M ops, 16 clients, 4 crashed ops live throughout)
+    at full size, against the oracle's pinned answer (hours on one core)."""
+    fx = _fixture("c5x")
+    h = synth.gen_config("c5x")
+    assert h.n == fx["n_entries"] and h.n_ops() == fx["n_ops"]
+    g = _lib.check(2, 0, h)
+    assert _ctab_count() == 1
+    assert int(g["valid"][0]) == fx["valid"] and int(g["explored"][0]) == fx["explored"]

@@ -1,6 +1,7 @@
 """Oracle pinning: the reference's golden vectors, hand KATs, and two independent
 restatements (brute-force linearization search, literal frozenset search)."""
 import json
+import sys
 import os
 import random
 
@@ -226,3 +227,23 @@ def test_c4_fixture_matches_generator():
     assert gold["valid"] == 1 and gold["explored"] == 10_994_841_001
     r = oracle.check_one("cas-register", synth.truncate(h, 4000))
     assert r["valid"] == 1 and r["explored"] > 0
+
+
+@pytest.mark.parametrize("name", ["c2c", "c2c4", "c5x"])
+def test_counter_fixtures_match_generator(name):
+    """tests/golden/counter_<name>_oracle.json (the oracle's whole-history counter search at size,
+    tests/golden/pin_counter.py) was made from this generator's history: same entry and op
+    counts and the same column digest; c2c (5 s on one core) is re-checked here in full."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import pin_counter
+    p = pin_counter.path_of(name)
+    if not os.path.exists(p):
+        pytest.skip(f"{name} not pinned yet")
+    gold = json.load(open(p))
+    h = pin_counter.GEN[name][1]()
+    assert (h.n, h.n_ops()) == (gold["n_entries"], gold["n_ops"])
+    assert pin_counter.digest(h) == gold["digest"]
+    assert gold["err_code"] == 0 and gold["valid"] in (0, 1)
+    if name == "c2c":
+        r = oracle.check_one("counter", h)
+        assert (r["valid"], r["explored"], r["fail_idx"]) == (gold["valid"], gold["explored"], gold["fail_idx"])
