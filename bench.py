@@ -376,6 +376,8 @@ def main():
                     help="cpu_baseline on every 20th key only (quick; the default is every key)")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="lc_check calls from host arrays timed after the run (0: skip)")
+    ap.add_argument("--e2e-shards", type=int, default=8,
+                    help="also time lc_check(n_gpus=S) from host arrays (0/1: skip)")
     ap.add_argument("--emulate", default="",
                     help="r/N: check rank r's share of an N-rank split on this one GPU")
     ap.add_argument("--partition", action="store_true",
@@ -492,6 +494,24 @@ def main():
                                        if k.startswith("create_")} | {
                                            "search_kernels": round(cs["kernel_ms"], 3)},
                "first_plan_create_phases_ms": phases}
+        if h.n_hist > 1 and args.e2e_shards > 1:
+            # lc_check(n_gpus = S) as a JVM caller spreads one independent history over S GPUs
+            # (register.clj:106): the batch is encoded once, split by modeled cost, each shard's
+            # plan copies its histories' encoded arrays; here the S shards are multiplexed on
+            # the visible device(s), so this is the host path plus S serialised searches
+            ref = _lib.check(kind, 0, h)
+            ts = []
+            for _ in range(args.e2e_reps):
+                t0 = time.perf_counter()
+                g = _lib.check(kind, 0, h, n_gpus=args.e2e_shards)
+                ts.append(time.perf_counter() - t0)
+            ts.sort()
+            same = all(np.array_equal(g[k], ref[k]) for k in ("valid", "fail_idx", "explored"))
+            e2e["sharded"] = {"n_gpus": args.e2e_shards, "devices": lc_devices(),
+                              "ms_per_check": ts[len(ts) // 2] * 1e3, "same_answers": bool(same),
+                              "what": "lc_check(n_gpus) multiplexed over the visible devices: one "
+                                      "encode, the cost split, per shard a copy of its encoded "
+                                      "histories + upload + search"}
 
     if dist:
         # every rank's explored configs (the whole job's configs/s)

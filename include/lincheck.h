@@ -35,7 +35,8 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 3  /* 2: lc_failure_configs gained last_op / out_last_op; 3: LC_MODEL_LEADER */
+#define LC_ABI_VERSION 4  /* 2: lc_failure_configs gained last_op / out_last_op; 3: LC_MODEL_LEADER;
+                            4: LC_H_ABORTED, statistics 34..38 (counter closure tables) */
 
 enum lc_model { LC_MODEL_CAS_REGISTER = 1, LC_MODEL_COUNTER = 2, LC_MODEL_LEADER = 3 };
 enum lc_valid { LC_INVALID = 0, LC_VALID = 1, LC_UNKNOWN = 2 };

@@ -168,7 +168,9 @@
       (throw (ex-info (c-string err) {:rc rc})))
     (vec (for [i (range k)]
            (let [ops (nth histories i)
-                 at  (fn [idx] (first (filter #(= idx (:index %)) ops)))
+                 ;; :index -> op, built once per history (was an O(n) filter per lookup)
+                 by-index (persistent! (reduce (fn [m op] (assoc! m (:index op) op)) (transient {}) ops))
+                 at  (fn [idx] (get by-index idx))
                  v   (aget valid i)]
              (cond-> {:valid?   (case v 1 true 0 false :unknown)
                       :analyzer :linear
@@ -182,9 +184,11 @@
                (and (zero? v) (:configs opts true))
                ((fn [r]
                   (if-let [{:keys [configs newest-last-op]}
-                           (cond-> (failure-configs i 10)
-                             (= 3 model-kind) (update :configs #(leader-config-models (:model opts) % ops
-                                                                                      (aget fail i))))]
+                           ;; (some->: no report (LC_E_CONFIGS) keeps the :previous-ok fallback)
+                           (some-> (failure-configs i 10)
+                                   (cond-> (= 3 model-kind)
+                                     (update :configs #(leader-config-models (:model opts) % ops
+                                                                             (aget fail i)))))]
                     (cond-> (assoc r
                                    :last-op (at newest-last-op)
                                    ;; Knossos :configs: {:model :last-op :pending}, :pending =

@@ -180,37 +180,48 @@ __device__ __forceinline__ uint64_t ct_x(const uint64_t* B, uint32_t w, uint32_t
 }
 
 // One step's closure of word w (its frontier X): the hi pulls and the in-word closure. Returns R.
+// Every LDS load that depends on w alone (the hi sums, the pulled words, their EQ bases) is
+// issued before any is used, then every EQ lookup (pulls and in-word gates) at once: a word's
+// chain is three LDS round trips (word list -> loads -> EQ) plus the VALU closure.
+constexpr int CT_PB = 4;  // pulls per batch (a word of popcount q <= CT_PB: one batch)
 __device__ __forceinline__ uint64_t ct_word(const uint64_t* Bt, uint32_t w, const CStep* st, uint32_t live, int j,
                                             uint64_t X) {
-  const int s_hi = (int)st->sh[0][w & 127u] + (int)st->sh[1][(w >> 7) & 127u];
   const bool jhi = j >= CTAB_LO;
   const uint32_t jh = jhi ? 1u << (j - CTAB_LO) : 0u;
-  uint32_t m = (w & jh) ? jh : w;
-  uint64_t R = 0;
-  while (m) {  // the word's set hi bits, two at a time (their loads issued together)
-    int b[2];
-    uint64_t v[2];
-    int32_t c[2];
+  const bool holds_j = (w & jh) != 0;
+  uint32_t m = holds_j ? jh : w;
+  const int sh0 = st->sh[0][w & 127u], sh1 = st->sh[1][(w >> 7) & 127u];
+  int32_t cl[CTAB_LO];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+  for (int k = 0; k < CTAB_LO; ++k) cl[k] = st->cq[k];  // (wave-uniform: the step's in-word ops)
+  uint64_t R = 0;
+  int s_hi = 0;
+  bool first = true;
+  do {  // the word's set hi bits, CT_PB at a time
+    int b[CT_PB];
+    uint64_t v[CT_PB];
+    int32_t c[CT_PB];
+#pragma unroll
+    for (int u = 0; u < CT_PB; ++u) {
       b[u] = m ? __builtin_ctz(m) : -1;
       m &= m - 1;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < CT_PB; ++u) {
       v[u] = b[u] >= 0 ? Bt[w ^ (1u << b[u])] : 0ull;
       c[u] = b[u] >= 0 ? st->cq[CTAB_LO + b[u]] : CQ_NEVER;
     }
+    if (first) s_hi = sh0 + sh1, first = false;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) R |= v[u] & gate(st, c[u], s_hi);
-  }
-  if (w & jh) return R;  // a word holding j (hi) is produced by linearizing j last only
+    for (int u = 0; u < CT_PB; ++u) R |= v[u] & gate(st, c[u], s_hi);
+  } while (m);
+  if (holds_j) return R;  // a word holding j (hi) is produced by linearizing j last only
   const uint64_t notj = jhi ? ~0ull : keep6(j);
   R &= notj;
   const uint32_t lo = live & 63u & ~(jhi ? 0u : 1u << j);
   uint64_t G[CTAB_LO];
 #pragma unroll
-  for (int k = 0; k < CTAB_LO; ++k) G[k] = ((live >> k) & 1u) ? gate(st, st->cq[k], s_hi) & keep6(k) & notj : 0ull;
+  for (int k = 0; k < CTAB_LO; ++k) G[k] = ((live >> k) & 1u) ? gate(st, cl[k], s_hi) & keep6(k) & notj : 0ull;
   for (;;) {  // the in-word closure: gated transfers until nothing changes
     const uint64_t R0 = R;
 #pragma unroll
@@ -308,6 +319,16 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
     unsigned long long expl = 0;
     int fail_t = -1;
     int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0;  // decoded, started, retired
+    // LC_DEBUG: super-layer phase cycles of wave 0 and of the decoder wave (s_memtime)
+    const bool prof = p.prof != nullptr && (tt == 0 || tt == CT_TEAM - 64);
+    unsigned long long ph[4] = {0, 0, 0, 0}, tp = prof ? __builtin_amdgcn_s_memtime() : 0, nsl = 0;
+    auto mark = [&](int k) {
+      if (prof) {
+        const unsigned long long tnow = __builtin_amdgcn_s_memtime();
+        ph[k] += tnow - tp;
+        tp = tnow;
+      }
+    };
     for (int s = 0; t_ret < ns; ++s) {
       // ---- ring view: lane i = step t_ret + i (decoded steps only)
       const int tl = t_ret + lane;
@@ -339,6 +360,8 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
       uint32_t nq_l = 0, o_l = 0;
       if (seg_l) nq_l = sBinom[h1.z * CT_BINOM + q_l], o_l = wofs[q_l];
       const uint64_t segm = __ballot(seg_l);
+      mark(0);
+      ++nsl;
       // the segments' words packed over the team, each padded to whole waves (every wave works
       // on a single step: its parameters are wave-uniform)
       uint32_t total = 0;
@@ -367,6 +390,7 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
         if (t > 0) st_fout += (uint32_t)__popcll(X);
         if (X) st->anyx = 1;
       }
+      mark(1);
       // ---- decode ahead into a slot nobody read in this super-layer
       const int t_dec_old = t_dec;
       if (t_dec < ns && t_dec - t_ret_old < CT_RING) {
@@ -391,7 +415,14 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
           ++t_run;
         }
       }
+      mark(2);
       __syncthreads();
+      mark(3);
+    }
+    if (prof) {
+      unsigned long long* q = p.prof + (tt == 0 ? 0 : 5);
+      for (int k = 0; k < 4; ++k) atomicAdd(&q[k], ph[k]);
+      atomicAdd(&q[4], nsl);
     }
     if (fail_t < 0 && ns > 0) {  // the last step's return
       const CStep* st = &sRing[(ns - 1) % CT_RING];

@@ -639,13 +639,14 @@ struct lc_plan {
   void wide_sink(int h, const HistView& v) {
     std::vector<uint32_t>& out = wide_streams[h];
     out.clear();
-    uint32_t live = 0;
+    uint64_t live = 0;
     int64_t q = 0;
     for (int64_t t = 0; t < v.n_steps; ++t) {
-      if (t > 0) live &= ~(1u << v.step_slot[t - 1]);
+      if (t > 0) live &= ~(1ull << v.step_slot[t - 1]);
       const int64_t q1 = q + v.step_ninv[t];
-      for (int64_t k = q; k < q1; ++k) live |= 1u << v.inv_slot[k];
-      out.push_back(live);
+      for (int64_t k = q; k < q1; ++k) live |= 1ull << v.inv_slot[k];
+      out.push_back((uint32_t)(live & 0x7fffffffu));
+      out.push_back((uint32_t)(live >> 31) & 0x7fffffffu);
       out.push_back((uint32_t)v.step_slot[t]);
       for (int64_t k = q; k < q1; ++k) {
         const int64_t a = v.inv_a[k], b = v.inv_b[k];
@@ -1699,6 +1700,9 @@ struct lc_plan {
       HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
       HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
       p.stamps = d_dstamps.as<unsigned long long>();
+      HIP_TRY(d_dlhist.ensure(16 * 8));
+      HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, 16 * 8, stream));
+      p.prof = d_dlhist.as<unsigned long long>();
     }
     const int grid = std::min(nc, dgrid_c);
     HIP_TRY(hipEventRecord(ev0, stream));
@@ -1750,6 +1754,14 @@ struct lc_plan {
                   enc.n_steps(h), (T[2 * h + 1] - T[2 * h]) / 100.0,
                   (T[2 * h + 1] - T[2 * h]) / 100.0 / std::max(1, enc.n_steps(h)));
         }
+      unsigned long long P[10];
+      if (hipMemcpy(P, d_dlhist.p, sizeof(P), hipMemcpyDeviceToHost) == hipSuccess)
+        for (int wv = 0; wv < 2; ++wv)
+          if (P[5 * wv + 4])
+            fprintf(stderr, "[lincheck]   %s: per super-layer cycles: ring %.0f words %.0f decode+start %.0f barrier %.0f "
+                    "(%llu super-layers)\n", wv ? "decoder wave" : "wave 0", P[5 * wv] / (double)P[5 * wv + 4],
+                    P[5 * wv + 1] / (double)P[5 * wv + 4], P[5 * wv + 2] / (double)P[5 * wv + 4],
+                    P[5 * wv + 3] / (double)P[5 * wv + 4], P[5 * wv + 4]);
     }
     return 0;
   }
@@ -1807,7 +1819,8 @@ struct lc_plan {
     p.anyv_off = (const int64_t*)((char*)d_wmeta.p + m_sb);
     p.nsteps = (const int32_t*)((char*)d_wmeta.p + 2 * m_sb);
     p.lmax = (const int8_t*)((char*)d_wmeta.p + 2 * m_sb + m_ns);
-    p.pipe = wide_pipe ? 1 : 0;
+    // (the one-step kernel's prefix tables stop at WIDE_NOPIPE_LMAX: wider tables always pipeline)
+    p.pipe = wide_pipe || lmax > WIDE_NOPIPE_LMAX ? 1 : 0;
     p.stream = d_wstream.as<uint32_t>();
     p.words = d_dwords.as<uint32_t>();
     p.tab = d_wtab.as<uint64_t>();
@@ -1865,11 +1878,11 @@ struct lc_plan {
       const std::vector<uint32_t>& ws = wide_streams[h];
       const int fs_i = fs[i];
       size_t q = 0;
-      for (int tt = 0; tt < enc.n_steps(h) && q + 1 < ws.size(); ++tt) {
+      for (int tt = 0; tt < enc.n_steps(h) && q + 2 < ws.size(); ++tt) {
         if (fs_i >= 0 && tt > fs_i + 1) break;
-        const int n = __builtin_popcount(ws[q] >> 3);
+        const int n = __builtin_popcountll(((uint64_t)ws[q] | ((uint64_t)ws[q + 1] << 31)) >> 3);
         alg += std::ldexp(1.0, n) * (n / 2.0 + 2.0) * 8.0;
-        q += 2;
+        q += 3;
         while (q < ws.size() && (ws[q] & DENSE_OPW)) ++q;
       }
     }
@@ -2512,21 +2525,25 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
             p->enc.live_max[0], DENSE_WIDE_LMAX);
     return LC_E_CONFIGS;
   }
-  if (p->enc.live_max[0] + p->state_bits_of(0) + 6 > 63) {
-    set_err(err, err_len, "failure configs unavailable: %d pending ops leave no room for the last-op tag",
-            p->enc.live_max[0]);
-    return LC_E_CONFIGS;
-  }
   // stop before the failing RETURN: the frontier it saw stays in flist (the grid kernel: the
-  // dense tables keep no config lists), each config tagged with the step that emitted it
-  p->max_t = t_fail;
-  p->report = true;
-  rc = p->run();
-  if (rc) {
-    set_err(err, err_len, "%s", p->last_error.c_str());
-    return rc;
-  }
-  if (p->status[0] != ST_RUNNING) {
+  // dense tables keep no config lists), each config tagged with the step that emitted it. A key
+  // with no room for the 6-bit tag, or a tagged frontier (a config once per route) that outgrows
+  // the lists, falls back to the untagged dump: the same configs, each with the
+  // previous :ok op as its :last-op (what the report shows without per-config tags)
+  bool tagged = p->enc.live_max[0] + p->state_bits_of(0) + 6 <= 63;
+  for (;;) {
+    p->max_t = t_fail;
+    p->report = tagged;
+    rc = p->run();
+    if (rc) {
+      set_err(err, err_len, "%s", p->last_error.c_str());
+      return rc;
+    }
+    if (p->status[0] == ST_RUNNING) break;
+    if (tagged) {
+      tagged = false;
+      continue;
+    }
     // the grid kernel's frontier lists overflowed before step t_fail (the verdict itself may
     // have come from the dense tables, which have no such limit): the lists are partial
     set_err(err, err_len, "failure configs unavailable: the pre-failure frontier of history %d exceeds the "
@@ -2571,7 +2588,7 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
       memcpy(&key, buf.data() + i * E, 8);
       int64_t val = 0;
       if (L.model != LC_MODEL_CAS_REGISTER) memcpy(&val, buf.data() + i * E + 8, 8);
-      const int tag = (int)((key >> tag_shift) & 63);
+      const int tag = tagged ? (int)((key >> tag_shift) & 63) : (t_fail - 1) & 63;  // untagged: age 0
       all.push_back({key & ((1ull << tag_shift) - 1), val, (t_fail - 1 - tag) & 63});
     }
   }

@@ -27,7 +27,7 @@ namespace lc {
 namespace {
 
 constexpr int WWG = 1024;
-constexpr int WB = 32;  // binomials C(n, k) for n < 32 (u32: C(31, 15) = 300,540,195)
+constexpr int WB = 33;  // binomials C(n, k) for n <= 32 (u32: C(32, 16) = 601,080,390)
 constexpr int WH = WIDE_LMAX - 3;  // most hi bits
 constexpr int WPRE = 513;          // per layer: prefix over <= 512 high parts, + the total
 
@@ -81,7 +81,7 @@ __device__ __forceinline__ bool wide_sync(const WideParams& p, int* sAbort) {
 // pulls of word w from T_t over its set bits (only j's when it holds j), eight loads in flight
 // per round: the loads are independent, so a round costs one HBM round trip
 __device__ __forceinline__ uint64_t wide_pulls(const uint64_t* B, uint32_t w, uint32_t jh, const OpSel* ops,
-                                              uint32_t foldm) {
+                                              uint64_t foldm) {
   uint32_t m = (w & jh) ? jh : w;
   uint64_t R = 0;
   while (m) {
@@ -105,8 +105,8 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
   __shared__ uint32_t sBin[WB * WB];
   __shared__ uint32_t sPre[(WH + 1) * WPRE];
   __shared__ uint32_t sLay[WIDE_LOW_BITS + 2];  // first entry of each popcount layer of the list
-  __shared__ OpSel sOps[32];                     // slot k's op
-  __shared__ uint32_t sHdr[4];                   // live, j, fresh, foldm
+  __shared__ OpSel sOps[WIDE_OPS];               // slot k's op
+  __shared__ uint64_t sHdr[4];                   // live, j, fresh, foldm
   __shared__ unsigned long long sRed;
   __shared__ int sAbort;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -136,34 +136,36 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
     // step 0 reads its frontier from tab(-1) = T1, at word 0 only (every slot is fresh there):
     // the initial config (register nil = state 0, nothing linearized)
     if (blockIdx.x == 0 && tid == 0) HbmTab::st(&T1[0], 1ull);
-    if (tid < 32) sOps[tid] = OpSel{SEL_NONE, SEL_NONE};
+    if (tid < WIDE_OPS) sOps[tid] = OpSel{SEL_NONE, SEL_NONE};
     if (!wide_sync(p, &sAbort)) break;
     unsigned long long expl = 0;
     int fail_t = -1, cH = -1, pj = -1;
-    uint32_t plive = 0;
+    uint64_t plive = 0;
     int64_t pos = p.sbeg[i];
     for (int t = 0; t < ns; ++t) {
       // ---- decode (wave 0 of every workgroup): 2 header words, then the op words
       if (tid < 64) {
         const uint32_t wd = p.stream[pos + lane];
-        const uint32_t live = (uint32_t)__shfl((int)wd, 0, 64), j = (uint32_t)__shfl((int)wd, 1, 64);
-        const unsigned long long ob = __ballot(lane >= 2 && lane < 2 + DENSE_MAX_NINV && (wd & DENSE_OPW));
-        const int ninv = (int)__builtin_ctzll(~(ob >> 2));
-        if (lane >= 2 && lane < 2 + ninv) sOps[wd & 31u] = decode_op((wd >> 8) & 0xffu, (wd >> 16) & 0xffu);
+        const uint64_t live = (uint64_t)(uint32_t)__shfl((int)wd, 0, 64) |
+                              ((uint64_t)(uint32_t)__shfl((int)wd, 1, 64) << 31);
+        const uint32_t j = (uint32_t)__shfl((int)wd, 2, 64);
+        const unsigned long long ob = __ballot(lane >= 3 && lane < 3 + DENSE_MAX_NINV && (wd & DENSE_OPW));
+        const int ninv = (int)__builtin_ctzll(~(ob >> 3));
+        if (lane >= 3 && lane < 3 + ninv) sOps[wd & 63u] = decode_op((wd >> 8) & 0xffu, (wd >> 16) & 0xffu);
         // (after the stores: one wave's LDS ops stay in order)
-        const uint32_t foldm = (uint32_t)__ballot(lane < 32 && sOps[lane & 31].hi == OPS_FOLD);
+        const uint64_t foldm = __ballot(lane < WIDE_OPS && sOps[lane < WIDE_OPS ? lane : 0].hi == OPS_FOLD);
         if (lane == 0) {
           sHdr[0] = live;
           sHdr[1] = j;
-          sHdr[2] = t > 0 ? live & ~(plive & ~(1u << pj)) : live;  // slots invoked since the last return
+          sHdr[2] = t > 0 ? live & ~(plive & ~(1ull << pj)) : live;  // slots invoked since the last return
           sHdr[3] = foldm;
         }
-        pos += 2 + ninv;
+        pos += 3 + ninv;
       }
       __syncthreads();
-      const uint32_t live = sHdr[0], fresh = sHdr[2], foldm = sHdr[3];
+      const uint64_t live = sHdr[0], fresh = sHdr[2], foldm = sHdr[3];
       const int j = (int)sHdr[1], jp = pj;
-      const int L = 32 - __clz((int)live);
+      const int L = 64 - __clzll((long long)live);
       const int H = L > 3 ? L - 3 : 0;
       const int k = H < WIDE_LOW_BITS ? H : WIDE_LOW_BITS, hb = H - k;
       if (H != cH) {  // layer q's prefix over the high parts: sPre[q][a] = sum_{a' < a} C(k, q - |a'|)
@@ -179,7 +181,7 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
         cH = H;
         __syncthreads();
       }
-      const uint32_t live_hi = live >> 3, fresh_hi = fresh >> 3;
+      const uint32_t live_hi = (uint32_t)(live >> 3), fresh_hi = (uint32_t)(fresh >> 3);
       const uint32_t jh = j >= 3 ? 1u << (j - 3) : 0u;
       uint64_t keep_lo = ~0ull;
 #pragma unroll
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
             X &= keep_lo;
           }
           uint64_t R = wide_pulls(B, w, jh, sOps, foldm);
-          R = close_in_word(X, w, live, j, sOps, foldm, R);
+          R = close_in_word(X, w, (uint32_t)live, j, sOps, (uint32_t)foldm, R);
           HbmTab::st(&B[w], X | R);
           expl += (uint64_t)__popcll(R);
           if (t > 0) st_fout += (uint64_t)__popcll(X);
@@ -227,13 +229,13 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
     }
     if (sAbort) break;
     if (fail_t < 0 && ns > 0) {  // the last step's return: its frontier must hold a config
-      const uint32_t lv = plive & ~(1u << pj);
-      const int Lf = lv ? 32 - __clz((int)lv) : 0;
+      const uint64_t lv = plive & ~(1ull << pj);
+      const int Lf = lv ? 64 - __clzll((long long)lv) : 0;
       const int64_t nwt = (int64_t)1 << (Lf > 3 ? Lf - 3 : 0);
       const uint64_t* const Bl = tab(ns - 1);
       uint64_t nz = 0;
       for (int64_t w = gtid; w < nwt; w += gstride) {
-        if ((uint32_t)w & ~(lv >> 3)) continue;
+        if ((uint64_t)w & ~(lv >> 3)) continue;
         uint64_t X;
         if (pj >= 3) X = HbmTab::ld(&Bl[(uint32_t)w | (1u << (pj - 3))]);
         else X = (HbmTab::ld(&Bl[w]) & ~keep64(pj)) >> (1 << pj);
@@ -281,9 +283,9 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
 // empty frontier.
 constexpr int WRING = 16;
 struct WStep {
-  OpSel ops[32];
-  uint32_t live, fresh, foldm, j;
-  int32_t jp, H, start, pad;
+  OpSel ops[WIDE_OPS];
+  uint64_t live, fresh, foldm;
+  int32_t j, jp, H, start;
 };
 
 __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
@@ -326,25 +328,27 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
       WStep* dst = &sRing[t % WRING];
       const WStep* prev = t > 0 ? &sRing[(t - 1) % WRING] : nullptr;
       const uint32_t wd = p.stream[pos + lane];
-      const uint32_t live = (uint32_t)__shfl((int)wd, 0, 64), j = (uint32_t)__shfl((int)wd, 1, 64);
-      const unsigned long long ob = __ballot(lane >= 2 && lane < 2 + DENSE_MAX_NINV && (wd & DENSE_OPW));
-      const int ninv = (int)__builtin_ctzll(~(ob >> 2));
-      const uint32_t plive = prev ? prev->live : 0u;
+      const uint64_t live = (uint64_t)(uint32_t)__shfl((int)wd, 0, 64) |
+                            ((uint64_t)(uint32_t)__shfl((int)wd, 1, 64) << 31);
+      const uint32_t j = (uint32_t)__shfl((int)wd, 2, 64);
+      const unsigned long long ob = __ballot(lane >= 3 && lane < 3 + DENSE_MAX_NINV && (wd & DENSE_OPW));
+      const int ninv = (int)__builtin_ctzll(~(ob >> 3));
+      const uint64_t plive = prev ? prev->live : 0ull;
       const int pj = prev ? (int)prev->j : -1;
-      if (lane < 32) dst->ops[lane] = prev ? prev->ops[lane] : OpSel{SEL_NONE, SEL_NONE};
-      if (lane >= 2 && lane < 2 + ninv) dst->ops[wd & 31u] = decode_op((wd >> 8) & 0xffu, (wd >> 16) & 0xffu);
-      const uint32_t foldm = (uint32_t)__ballot(lane < 32 && dst->ops[lane & 31].hi == OPS_FOLD);
+      if (lane < WIDE_OPS) dst->ops[lane] = prev ? prev->ops[lane] : OpSel{SEL_NONE, SEL_NONE};
+      if (lane >= 3 && lane < 3 + ninv) dst->ops[wd & 63u] = decode_op((wd >> 8) & 0xffu, (wd >> 16) & 0xffu);
+      const uint64_t foldm = __ballot(lane < WIDE_OPS && dst->ops[lane < WIDE_OPS ? lane : 0].hi == OPS_FOLD);
       if (lane == 0) {
-        const int L = 32 - __clz((int)live);
+        const int L = 64 - __clzll((long long)live);
         dst->live = live;
-        dst->fresh = prev ? live & ~(plive & ~(1u << pj)) : live;
+        dst->fresh = prev ? live & ~(plive & ~(1ull << pj)) : live;
         dst->foldm = foldm;
-        dst->j = j;
+        dst->j = (int32_t)j;
         dst->jp = pj;
         dst->H = L > 3 ? L - 3 : 0;
         dst->start = 1 << 30;
       }
-      pos += 2 + ninv;
+      pos += 3 + ninv;
     };
     if (ns > 0) decode(0);
     __syncthreads();
@@ -395,9 +399,9 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
         const uint32_t nlo = sBin[k * WB + (q - pp)];
         const uint32_t hi_i = gi / nlo, lo_i = gi - hi_i * nlo;
         const uint32_t w = (hb ? (p.words[sLay[pp] + hi_i] << k) : 0u) | p.words[sLay[q - pp] + lo_i];
-        const uint32_t live = r.live;
-        if (w & ~(live >> 3)) continue;
-        const uint32_t fresh = r.fresh, foldm = r.foldm;
+        const uint64_t live = r.live;
+        if ((uint64_t)w & ~(live >> 3)) continue;
+        const uint64_t fresh = r.fresh, foldm = r.foldm;
         const int j = (int)r.j, jp = r.jp;
         uint64_t X = 0;
         if (!(w & (fresh >> 3))) {
@@ -411,7 +415,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
         }
         uint64_t* const B = tab(t);
         uint64_t R = wide_pulls(B, w, j >= 3 ? 1u << (j - 3) : 0u, r.ops, foldm);
-        R = close_in_word(X, w, live, j, r.ops, foldm, R);
+        R = close_in_word(X, w, (uint32_t)live, j, r.ops, (uint32_t)foldm, R);
         HbmTab::st(&B[w], X | R);
         expl += (uint64_t)__popcll(R);
         if (t > 0) st_fout += (uint64_t)__popcll(X);
@@ -450,13 +454,13 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
     if (fail_t < 0 && ns > 0) {  // the last step's return: its frontier must hold a config
       const WStep& r = sRing[(ns - 1) % WRING];
       const int pj = (int)r.j;
-      const uint32_t lv = r.live & ~(1u << pj);
-      const int Lf = lv ? 32 - __clz((int)lv) : 0;
+      const uint64_t lv = r.live & ~(1ull << pj);
+      const int Lf = lv ? 64 - __clzll((long long)lv) : 0;
       const int64_t nwt = (int64_t)1 << (Lf > 3 ? Lf - 3 : 0);
       const uint64_t* const Bl = tab(ns - 1);
       uint64_t nz = 0;
       for (int64_t w = gtid; w < nwt; w += gstride) {
-        if ((uint32_t)w & ~(lv >> 3)) continue;
+        if ((uint64_t)w & ~(lv >> 3)) continue;
         uint64_t X;
         if (pj >= 3) X = HbmTab::ld(&Bl[(uint32_t)w | (1u << (pj - 3))]);
         else X = (HbmTab::ld(&Bl[w]) & ~keep64(pj)) >> (1 << pj);

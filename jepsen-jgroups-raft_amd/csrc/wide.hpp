@@ -14,12 +14,15 @@
 
 namespace lc {
 
-constexpr int WIDE_LMAX = 31;       // widest history: 2 tables of 2^28 words (4 GiB); slots <= 30 keep bit 31 of a stream header clear
+constexpr int WIDE_LMAX = 35;       // widest history: 2 tables of 2^32 words (64 GiB of the 288 GB HBM)
+constexpr int WIDE_NOPIPE_LMAX = 31;  // the one-step-at-a-time kernel's layer prefix tables stop here
+constexpr int WIDE_OPS = 36;        // op-table entries per step (slots 0..34, + the pull loop's reads)
 constexpr int WIDE_LOW_BITS = 19;   // a layer's words = high part x low part from the sorted list
 
 // Step stream of a wide history (host-built, its own buffer):
-//   header word 0  live (bits 0..30), bit 31 clear
-//   header word 1  j (the returning slot), bit 31 clear
+//   header word 0  live slots 0..30, bit 31 clear
+//   header word 1  live slots 31..61 (bit k - 31), bit 31 clear
+//   header word 2  j (the returning slot), bit 31 clear
 //   op words, one per invocation since the previous step (<= DENSE_MAX_NINV), bit 31 set:
 //                  slot[0:8) | amask[8:16) | bmask[16:24) | DENSE_OPW
 //   a 0 word after the last step

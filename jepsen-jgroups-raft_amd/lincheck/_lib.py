@@ -20,7 +20,7 @@ EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_release", "lc_ch
            "lc_bounds_plan_run", "lc_bounds_plan_destroy", "lc_part_create", "lc_part_info",
            "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
            "lc_part_step_end", "lc_part_results", "lc_part_run", "lc_part_destroy", "lc_part_check")
-ABI_VERSION = 3
+ABI_VERSION = 4
 STATS_N = 39
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",

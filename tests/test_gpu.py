@@ -241,6 +241,26 @@ def test_gpu_failure_configs_match_oracle(m):
     assert found > 5 and carried > 0  # some configs were carried through the last RETURN
 
 
+def test_gpu_failure_configs_untagged_fallback():
+    """a key with no room for the 6-bit last-op tag (here 56 calls pending + 3 state
+    bits) still gets its :configs, untagged: the same configs as the oracle's, each with the
+    previous :ok op as its :last-op (the report's no-tag rendering)."""
+    for t in range(8):
+        base = synth.gen_register(40, 3, 0.0, 9100 + t, invalid=True)
+        h = _with_never_ops(base, 52)
+        g = _lib.check(1, 0, h)
+        e = oracle.check_one("cas-register", h, with_configs=True)
+        assert int(g["valid"][0]) == e["valid"]
+        if e["valid"] != 0:
+            continue
+        cfgs, pending, lasts, newest = _lib.failure_configs(0, 1 << 12, with_last=True)
+        assert set(cfgs) == e["fail_configs"] and len(cfgs) == len(e["fail_configs"])
+        assert sorted(pending) == sorted(e["pending_inv_idx"])
+        assert all(x == e["prev_ok_idx"] for x in lasts) and newest == e["prev_ok_idx"]
+        return
+    pytest.fail("no invalid history among the seeds")
+
+
 def _leader_hists(n, seed0, n_ops=200, p_crash=0.03):
     return [synth.gen_leader(n_ops, 5, 0.05, seed0 + t, invalid=(t % 3 == 1), n_terms=4 + t % 5,
                              p_crash=p_crash if t % 2 else 0.0) for t in range(n)]
@@ -1125,6 +1145,30 @@ def test_gpu_wide_tables_past_the_tile_teams():
     g = _lib.check(1, 0, h)
     assert _lib.check_stats()["wide_histories"] == 1
     assert int(g["valid"][0]) == 1 and int(g["explored"][0]) > 0
+
+
+def test_gpu_wide_tables_past_31_slots():
+    """r4: the HBM tables up to live width 35 (2 x 2^32 words = 64 GiB),
+    stream headers with 64-bit live masks. Small bases with up to 32 calls pending throughout
+    that can never apply (so the oracle stays fast while the tables reach 2^29..2^32 words per
+    step), valid and with a read of a value never written, against the oracle."""
+    for base_ops, clients, n, bad, seed in ((60, 4, 28, False, 57000), (60, 4, 29, True, 57001),
+                                            (40, 3, 31, False, 57002), (30, 3, 32, True, 57003)):
+        base = synth.gen_register(base_ops, clients, 0.0, seed)
+        if bad:
+            reads = [i for i in range(base.n) if base.type[i] == 1 and base.f[i] == 0 and base.vflags[i] == H.V_SCALAR]
+            if reads:
+                v0 = base.v0.copy()
+                v0[reads[len(reads) // 2]] = 7
+                base = H.from_columns(base.index, base.process, base.type, base.f, v0, base.v1, base.vflags)
+        h = _with_never_ops(base, n)
+        w = _live_width(h, 0)
+        assert 31 < w <= 35, w
+        g = _lib.check(1, 0, h)
+        assert _lib.check_stats()["wide_histories"] == 1, w
+        e = oracle.check_one("cas-register", h)
+        _cmp(g, e, 0, f"wide w={w}")
+        assert int(g["explored"][0]) == oracle.check_one("cas-register", base)["explored"]
 
 
 def test_gpu_wide_watchdog_abort_is_unknown(monkeypatch):

@@ -3,7 +3,7 @@
 # infrastructure event (exit 3: nothing ran, nothing charged). Any other outcome returns.
 # usage: tools/gpu.sh <timeout_s> '<command>'
 to=$1; shift
-for i in 1 2 3 4 5 6 7 8; do
+for i in $(seq 1 ${GPU_RETRIES:-8}); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@"
   rc=$?
   [ $rc -ne 3 ] && exit $rc
