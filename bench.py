@@ -570,6 +570,15 @@ def main():
                          "configs explored (lower bound)" if table_hbm is not None else
                          "SURVEY 8(d): F_in*C + N_cand*(C+8) + F_out*C",
             "terms": {"frontier_in": fin, "n_cand": expl, "frontier_out": fout}}
+    if avg.get("slowest_history_us", 0) > 0 and k_ms > 0:
+        # how much of the launch is ONE history's dependent chain of steps
+        # (its dequeue-to-end time on the device clock): near 1, the kernel is chain-bound and
+        # the nominal §8(d) frac says little about it
+        sh_ms = avg["slowest_history_us"] / 1e3
+        roof["chain"] = {"slowest_history_ms": sh_ms, "steps": int(st["slowest_history_steps"]),
+                         "width": int(st["slowest_history_width"]),
+                         "us_per_step": avg["slowest_history_us"] / max(1.0, st["slowest_history_steps"]),
+                         "frac_of_kernel": sh_ms / k_ms}
     if table_hbm is not None:
         lds_ach = lds_bytes / k_s / 1e9 if k_s > 0 else 0.0
         roof["table"] = {"hbm_bytes_per_launch": table_hbm, "lds_bytes_per_launch": lds_bytes,

@@ -222,8 +222,11 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  * 33 their algorithmic HBM bytes: per step and live word, its X, its pulls and its store (8 B each)
  * 34 counter histories decided on closure tables (ctab.hip; counted in 12 too)  35 their kernel's ms
  * 36..38 the counter tables' frontier configs in, frontier configs out, configs explored
+ * 39..41 the closure-table kernels' slowest history: its microseconds from dequeue to end (device
+ *    clock), its RETURN steps, its live width (a launch bound by one history's chain of steps
+ *    lasts about that long)
  */
-#define LC_STATS_N 39
+#define LC_STATS_N 42
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
 void lc_plan_destroy(lc_plan* p);
 

@@ -1017,12 +1017,12 @@ struct lc_plan {
     p.fail_step = d_dfail.as<int32_t>();
     p.explored = d_dexpl.as<unsigned long long>();
     p.stats = d_stats.as<unsigned long long>();
-    p.stamps = nullptr;
     p.pipe = dense_pipe;
+    // per-history start / end stamps (always: the chain-bound figure, stats 39..41)
+    HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
+    z0.add(d_dstamps.p, (size_t)std::max(n, 1) * 32);
+    p.stamps = d_dstamps.as<unsigned long long>();
     if (debug()) {
-      HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
-      HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
-      p.stamps = d_dstamps.as<unsigned long long>();
       HIP_TRY(d_dlhist.ensure((64 * LH_N + 32) * 8));
       HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, (64 * LH_N + 32) * 8, stream));
       p.lhist = d_dlhist.as<unsigned long long>();
@@ -1237,7 +1237,7 @@ struct lc_plan {
     *ms += t;
     // the results (explored, status, fail step, stats, abort word) into one pinned buffer,
     // copied back-to-back and waited on once
-    const size_t need = (size_t)n * 16 + 3 * SS_N * 8 + 16;
+    const size_t need = (size_t)n * 48 + 3 * SS_N * 8 + 16;
     if (hstage_bytes < need) {
       if (hstage) HIP_TRY(hipHostFree(hstage));
       hstage = nullptr;
@@ -1249,6 +1249,8 @@ struct lc_plan {
     int32_t* const fs = st + n;
     unsigned long long* const ss3 = reinterpret_cast<unsigned long long*>(fs + n);  // (16 n bytes in)
     int32_t* const abw = reinterpret_cast<int32_t*>(ss3 + 3 * SS_N);
+    unsigned long long* const stamp = reinterpret_cast<unsigned long long*>(ss3 + 3 * SS_N + 2);
+    HIP_TRY(hipMemcpyAsync(stamp, d_dstamps.p, (size_t)n * 32, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(ex, d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st, d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(fs, d_dfail.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
@@ -1263,7 +1265,10 @@ struct lc_plan {
     unsigned long long ss[SS_N];
     for (int i = 0; i < SS_N; ++i) ss[i] = ss3[i] + ss3[SS_N + i] + ss3[2 * SS_N + i];
     for (const std::vector<int>* ids : {&dense_b, &dense_w, &dense_x, &dense_m})
-      for (int h : *ids) status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
+      for (int h : *ids) {
+        status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
+        note_chain(h, stamp[4 * h], stamp[4 * h + 1]);
+      }
     stats[1] += (nw && !wave_in_big ? 1 : 0) + (nm && !mid_in_big ? 1 : 0) + (double)launches.size();
     stats[12] += nb + nw + nx + nm;
     stats[13] += t;
@@ -1669,6 +1674,15 @@ struct lc_plan {
     return free_b;
   }
 
+  // The slowest history of the run (device clock stamps at its dequeue and its end, 100 MHz):
+  // stats 39..41 = its microseconds, RETURN steps and live width. Against the kernel time it
+  // says how much of the launch is one history's dependent chain of steps.
+  void note_chain(int h, unsigned long long t0, unsigned long long t1) {
+    if (!t0 || t1 < t0) return;
+    const double us = (double)(t1 - t0) / 100.0;
+    if (us > stats[39]) stats[39] = us, stats[40] = enc.n_steps(h), stats[41] = enc.live_max[h];
+  }
+
   // Counter histories on closure tables (ctab.hip): one launch, one history per 1024-thread
   // workgroup (dequeued heaviest first), their step streams already in d_dpack.
   int run_ctab(float* ms) {
@@ -1696,10 +1710,10 @@ struct lc_plan {
     p.explored = d_dexpl.as<unsigned long long>();
     p.stats = d_cstats.as<unsigned long long>();
     p.pipe = ctab_pipe;
+    HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
+    HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
+    p.stamps = d_dstamps.as<unsigned long long>();
     if (debug()) {
-      HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
-      HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
-      p.stamps = d_dstamps.as<unsigned long long>();
       HIP_TRY(d_dlhist.ensure(16 * 8));
       HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, 16 * 8, stream));
       p.prof = d_dlhist.as<unsigned long long>();
@@ -1708,7 +1722,7 @@ struct lc_plan {
     HIP_TRY(hipEventRecord(ev0, stream));
     HIP_TRY(launch_ctab(p, grid, stream));
     HIP_TRY(hipEventRecord(ev1, stream));
-    const size_t need = (size_t)n * 16 + 16;
+    const size_t need = (size_t)n * 32 + 16;
     if (hstage_bytes < need) {
       if (hstage) HIP_TRY(hipHostFree(hstage));
       hstage = nullptr;
@@ -1719,6 +1733,8 @@ struct lc_plan {
     int32_t* const st = reinterpret_cast<int32_t*>(hstage + n);
     int32_t* const fs = st + n;
     unsigned long long* const cs = reinterpret_cast<unsigned long long*>(fs + n);
+    unsigned long long* const stamp = cs + 2;  // [n][2]
+    HIP_TRY(hipMemcpyAsync(stamp, d_dstamps.p, (size_t)n * 16, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(ex, d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(st, d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipMemcpyAsync(fs, d_dfail.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
@@ -1731,6 +1747,7 @@ struct lc_plan {
     for (int h : dense_c) {
       status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
       expl += (double)ex[h];
+      note_chain(h, stamp[2 * h], stamp[2 * h + 1]);
     }
     stats[1] += 1;
     stats[2] += (double)cs[1];

@@ -21,7 +21,7 @@ EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_release", "lc_ch
            "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
            "lc_part_step_end", "lc_part_results", "lc_part_run", "lc_part_destroy", "lc_part_check")
 ABI_VERSION = 4
-STATS_N = 39
+STATS_N = 42
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
                "spill_inserts", "dense_histories", "dense_ms", "dense_big_ms", "dense_wave_ms",
@@ -31,7 +31,8 @@ STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candi
                "dense_big_frontier_in", "dense_big_frontier_out", "dense_big_explored",
                "dense_wave_frontier_in", "dense_wave_frontier_out", "dense_wave_explored",
                "wide_histories", "wide_ms", "wide_hbm_bytes",
-               "ctab_histories", "ctab_ms", "ctab_frontier_in", "ctab_frontier_out", "ctab_explored")
+               "ctab_histories", "ctab_ms", "ctab_frontier_in", "ctab_frontier_out", "ctab_explored",
+               "slowest_history_us", "slowest_history_steps", "slowest_history_width")
 
 P = C.c_void_p
 I8P = C.POINTER(C.c_int8)

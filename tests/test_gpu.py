@@ -103,6 +103,15 @@ def test_gpu_c2_full_size_vs_oracle():
     _cmp(g, oracle.check_one("cas-register", h), 0, "c2-full")
 
 
+def test_gpu_c2_full_size_x_prefetch(monkeypatch):
+    """C2 at full size with LC_PIPE bit 19 (r4): a tile team's X words of the next super-layer
+    loaded from other tiles' mirrors at the end of the current one; bit-exact with the oracle."""
+    monkeypatch.setenv("LC_PIPE", str(217039 | 524288))
+    h = synth.gen_config("c2")
+    g = _lib.check(1, 0, h)
+    _cmp(g, oracle.check_one("cas-register", h), 0, "c2-xpre")
+
+
 # C4 (BASELINE configs[3]): one 100k-op history with crashed :info ops. Its full-size oracle
 # verdict and explored count (tests/golden/c4_oracle.json: the C oracle on one thread, 3.0 h,
 # made by tests/golden/pin_c4.py) are the fixture every GPU path must reproduce.
@@ -702,8 +711,8 @@ def test_gpu_dense_tile_teams_small_tiles(lbits, monkeypatch):
     p.close()
 
 
-@pytest.mark.parametrize("pipe", ["207", "463", "719", "975"],
-                         ids=["tokens", "tagged", "tokens-dbl", "tagged-dbl"])
+@pytest.mark.parametrize("pipe", ["207", "463", "719", "975", "525263"],
+                         ids=["tokens", "tagged", "tokens-dbl", "tagged-dbl", "tagged-dbl-xpre"])
 @pytest.mark.parametrize("rot,lbits", [("1", "14"), ("3", "13"), ("9", "15"), ("9", None)])
 def test_gpu_dense_tile_teams_rotated(rot, lbits, pipe, monkeypatch):
     """LC_TEAM_ROT: a tile team's lowest slots relabelled as its team bits (every tile holds a

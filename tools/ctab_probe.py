@@ -11,6 +11,10 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "jepsen-jgroups-raft_amd"), os.path.join(ROOT, "oracle")]
+for a in list(sys.argv[1:]):  # lib=<suffix>: an A/B build lincheck/liblincheck_<suffix>.so
+    if a.startswith("lib="):
+        os.environ["LC_LIB"] = os.path.join(ROOT, "jepsen-jgroups-raft_amd", "lincheck", f"liblincheck_{a[4:]}.so")
+        sys.argv.remove(a)
 
 import oracle  # noqa: E402  (checker of the spot checks)
 from lincheck import _lib, history as H, synth  # noqa: E402
@@ -59,7 +63,7 @@ def main(cases):
             g, t, st = timed(h, reps=3 if name != "c5x" else 2)
             os.environ.pop("LC_CTAB_MAXW", None)
             fx = fixture(name)
-            print(json.dumps({"case": c, "ops": h.n_ops(), "valid": int(g["valid"][0]),
+            print(json.dumps({"case": c, "lib": os.environ.get("LC_LIB", "default"), "ops": h.n_ops(), "valid": int(g["valid"][0]),
                               "explored": int(g["explored"][0]),
                               "fixture_explored": fx and fx["explored"],
                               "match": fx is not None and int(g["explored"][0]) == fx["explored"] and
