@@ -1254,6 +1254,18 @@ constexpr int PIPE_WSPREAD = 262144;  // big kernel: WAVE histories one per work
 // an early read safe: a word not yet written is polled); a prefetched value is used only when its
 // (step, word) matches the word the wave then takes.
 constexpr int PIPE_XPRE = 524288;
+// LC_PIPE bit 20 (r4): tagged tile teams end a super-layer with an LDS-only barrier (a release /
+// acquire fence on the local address space around s_barrier): the LDS tables and the ring are
+// all a super-layer hands to the next within a workgroup, the mirror words travel with their
+// tags, so the barrier need not wait for this super-layer's mirror stores (s_waitcnt vmcnt(0))
+// nor for loads already issued for the next one (PIPE_XPRE)
+constexpr int PIPE_LBAR = 1048576;
+
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 __device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
                                            unsigned long long need, uint64_t t0, long& spins) {
@@ -1340,8 +1352,9 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   static_assert((1 << DENSE_TEAM_MAXB) <= 4 * 64, "credit pre-poll registers");
   // PIPE_XPRE: X words loaded a super-layer ahead (the packed loop's first pass)
   const bool xpre_on = (p.pipe & PIPE_XPRE) && tagged && !(p.pipe & PIPE_SERIAL_SEGS);
-  uint64_t xpre = 0;
+  uint64_t xga = 0, xgb = 0;  // the two tagged granules, loaded without waiting (checked at use)
   uint32_t xkey = ~0u;  // (step << 12 | word row) the value belongs to
+  const bool lbar = (p.pipe & PIPE_LBAR) && tagged;
   for (int s = 0; t_ret < ns; ++s) {
     unsigned long long tp = timed ? now() : 0;
     if (s >= cw && (s & (cw - 1)) == 0) {  // credit: nobody more than cw super-layers behind
@@ -1483,9 +1496,11 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         const bool pl = tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u));
         if (tagged) {
           if (fx && xs >= 0) {
-            const uint32_t key = ((uint32_t)t << 12) | r;
-            xv = (xpre_on && f0 < 1024u && xkey == key) ? xpre
-                                                        : TagTab::ld(mirror(xs, t - 1), mp + r, tag_of(t - 1), p.abort);
+            const uint32_t key = ((uint32_t)t << 12) | r, tg = tag_of(t - 1);
+            if (xpre_on && f0 < 1024u && xkey == key && (uint32_t)(xga >> 32) == tg && (uint32_t)(xgb >> 32) == tg)
+              xv = (uint32_t)xga | (xgb << 32);
+            else
+              xv = TagTab::ld(mirror(xs, t - 1), mp + r, tg, p.abort);
           }
 #pragma unroll
           for (int b = 0; b < TB; ++b)
@@ -1683,13 +1698,17 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         const bool tile_fresh = ((uint32_t)rank & (fresh >> lb)) != 0;
         if (tile_fresh || (w & ((fresh & lmask) >> 3))) break;
         const int t = t_ret_old + i;
-        xpre = TagTab::ld(mirror(xs, t - 1), rdl(mp1, i) + r, tag_of(t - 1), p.abort);
+        const uint64_t* slot = mirror(xs, t - 1);
+        const uint32_t wi = rdl(mp1, i) + r;
+        xga = HbmTab::ld(&slot[2 * wi]);  // (issued now, waited for where they are used)
+        xgb = HbmTab::ld(&slot[2 * wi + 1]);
         xkey = ((uint32_t)t << 12) | r;
       } while (false);
     }
     if (timed) ph[1] += now() - tp, tp = now();
     if (wide_any && !tagged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-    __syncthreads();
+    if (lbar) lds_barrier();
+    else __syncthreads();
     if (tid == 0) st_agent(&flags[rank], (unsigned long long)(s + 1));
     if (timed) ph[2] += now() - tp, ph[5] += 1;
   }

@@ -103,13 +103,15 @@ def test_gpu_c2_full_size_vs_oracle():
     _cmp(g, oracle.check_one("cas-register", h), 0, "c2-full")
 
 
-def test_gpu_c2_full_size_x_prefetch(monkeypatch):
-    """C2 at full size with LC_PIPE bit 19 (r4): a tile team's X words of the next super-layer
-    loaded from other tiles' mirrors at the end of the current one; bit-exact with the oracle."""
-    monkeypatch.setenv("LC_PIPE", str(217039 | 524288))
+@pytest.mark.parametrize("bits", [524288, 1048576, 524288 | 1048576], ids=["xpre", "lbar", "xpre-lbar"])
+def test_gpu_c2_full_size_x_prefetch(bits, monkeypatch):
+    """C2 at full size with LC_PIPE bits 19/20 (r4): a tile team's X words of the next
+    super-layer issued from other tiles' mirrors at the end of the current one (checked by
+    their tags where used), and the super-layer's LDS-only barrier; bit-exact with the oracle."""
+    monkeypatch.setenv("LC_PIPE", str(217039 | bits))
     h = synth.gen_config("c2")
     g = _lib.check(1, 0, h)
-    _cmp(g, oracle.check_one("cas-register", h), 0, "c2-xpre")
+    _cmp(g, oracle.check_one("cas-register", h), 0, f"c2-pipe-{bits}")
 
 
 # C4 (BASELINE configs[3]): one 100k-op history with crashed :info ops. Its full-size oracle
@@ -711,8 +713,8 @@ def test_gpu_dense_tile_teams_small_tiles(lbits, monkeypatch):
     p.close()
 
 
-@pytest.mark.parametrize("pipe", ["207", "463", "719", "975", "525263"],
-                         ids=["tokens", "tagged", "tokens-dbl", "tagged-dbl", "tagged-dbl-xpre"])
+@pytest.mark.parametrize("pipe", ["207", "463", "719", "975", "525263", "1573839"],
+                         ids=["tokens", "tagged", "tokens-dbl", "tagged-dbl", "tagged-dbl-xpre", "tagged-dbl-xpre-lbar"])
 @pytest.mark.parametrize("rot,lbits", [("1", "14"), ("3", "13"), ("9", "15"), ("9", None)])
 def test_gpu_dense_tile_teams_rotated(rot, lbits, pipe, monkeypatch):
     """LC_TEAM_ROT: a tile team's lowest slots relabelled as its team bits (every tile holds a

@@ -10,6 +10,7 @@
 #   trace:<name>:<bench args>     rocprofv3 --kernel-trace --stats over bench.py <args>
 #   pmc:<name>:<ctrs>:<bench args> rocprofv3 --pmc <ctrs> (commas -> spaces) over bench.py <args>
 #   py:<name>:<script args>       python -u <script args> > <name>.log
+#   env:<VAR>=<value>             export VAR for the steps after it (env:<VAR>= unsets it)
 # e.g. tools/run.sh r4a 'test:tests/test_gpu_counter.py' 'bench:c2c:--workload,c2c,--steps,5'
 set -o pipefail
 tag=$1
@@ -42,6 +43,9 @@ for step in "$@"; do
     py)
       name=${rest%%:*}; args=$(sp "${rest#*:}")
       timeout -k 10 900 python -u $args > "$out/$name.log" 2>&1 || { echo "[run.sh] FAILED $step"; tail -5 "$out/$name.log"; exit 1; } ;;
+    env)
+      var=${rest%%=*}; val=${rest#*=}
+      if [ -n "$val" ]; then export "$var=$val"; else unset "$var"; fi ;;
     *) echo "[run.sh] unknown step $step"; exit 2 ;;
   esac
 done
