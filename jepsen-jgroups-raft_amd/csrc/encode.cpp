@@ -38,7 +38,7 @@ struct Op {
   int8_t status;  // -1 pending forever, else completion type
   int8_t f, vflags;
   uint8_t slot;
-  uint8_t inword;  // slot policy: chosen for an in-word slot (0..2)
+  uint8_t inword;  // slot policy: chosen for an in-word slot (0..2; a counter's 0..5)
   uint8_t kind;    // model operands (computed once, before the assignment pass)
   int64_t oa, ob;
 };
@@ -138,7 +138,10 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
     const char* e = getenv("LC_SLOTS");
     return e && strcmp(e, "lff") == 0;
   }();
-  int64_t mfree[3] = {-1, -1, -1};
+  // in-word slots: 3 for the register tables' words (8 masks x 8 states), 6 for the counter
+  // tables' (64 masks, ctab.hpp)
+  const int n_iw = model == LC_MODEL_COUNTER ? 6 : 3;
+  int64_t mfree[6] = {-1, -1, -1, -1, -1, -1};
   // ---- pairing (knossos.history [ext])
   ops.clear();
   std::vector<int32_t>& op_of = sc.op_of;
@@ -169,7 +172,7 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
           op.v1 = a.v1[i];
           n_ok++;
           int best = -1;  // slot policy: the machine free latest before this op's invocation
-          for (int m = 0; m < 3; ++m)
+          for (int m = 0; m < n_iw; ++m)
             if (mfree[m] < op.inv_pos && (best < 0 || mfree[m] > mfree[best])) best = m;
           if (best >= 0) op.inword = 1, mfree[best] = i;
         }
@@ -354,10 +357,10 @@ void encode_one(int model, const HistArrays& a, int64_t b, int64_t e, OneOut& o)
         break;
       }
       int sl = __builtin_ctzll(~used);
-      if (sl < 3 && !op.inword && !slots_lff) {
-        const int hi = __builtin_ctzll(~(used | 7ull));  // the lowest free slot >= 3
+      if (sl < n_iw && !op.inword && !slots_lff) {
+        const int hi = __builtin_ctzll(~(used | ((1ull << n_iw) - 1)));  // the lowest free slot >= n_iw
         const int npend = __builtin_popcountll(used) + 1;
-        if (hi < std::max(npend, 3)) sl = hi;  // (no wider than lowest-free-first)
+        if (hi < std::max(npend, n_iw)) sl = hi;  // (no wider than lowest-free-first)
       }
       used |= 1ull << sl;
       op.slot = (uint8_t)sl;

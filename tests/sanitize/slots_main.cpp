@@ -10,7 +10,10 @@
 #include "../../jepsen-jgroups-raft_amd/csrc/encode.hpp"
 #include "../../include/lincheck.h"
 
-int main() {
+// argv[1] = "counter": CounterModel histories (read / add / add-and-get), in-word slots 0..5
+int main(int argc, char** argv) {
+  const bool counter = argc > 1 && argv[1][0] == 'c';
+  const int n_iw = counter ? 6 : 3;
   std::mt19937_64 rng(0x51075);
   for (int it = 0; it < 400; ++it) {
     // one history: nproc clients, each with one op in flight; :info makes a fresh process, :fail
@@ -29,13 +32,15 @@ int main() {
       const int p = (int)(rng() % nproc);
       const int64_t a = (int64_t)(rng() % 4), b = (int64_t)(rng() % 4);
       if (open[p] < 0) {
-        const int ff = (int)(rng() % 3);
-        add(pid[p], 0, ff, ff == 2 ? 2 : ff == 0 ? 0 : 1, a, b);
+        int ff = (int)(rng() % 3);
+        if (counter) ff = ff == 0 ? 0 : ff == 1 ? 3 : 5;  // read / add / add-and-get
+        add(pid[p], 0, ff, counter ? (ff == 0 ? 0 : 1) : (ff == 2 ? 2 : ff == 0 ? 0 : 1), a, b);
         open[p] = ff;
       } else {
         const int r = (int)(rng() % 20);
         const int t = r < 17 ? 1 : r < 19 ? 2 : 3;
-        add(pid[p], t, open[p], open[p] == 2 ? 2 : 1, a, b);
+        const int vf = counter ? (open[p] == 5 && t == 1 ? 2 : 1) : (open[p] == 2 ? 2 : 1);
+        add(pid[p], t, open[p], vf, a, b);
         open[p] = -1;
         if (t == 3) pid[p] += nproc;
       }
@@ -44,14 +49,14 @@ int main() {
     lc::HistArrays h{off[1], index.data(), process.data(), type.data(), f.data(), v0.data(), v1.data(),
                      vflags.data()};
     lc::Encoded enc;
-    lc::encode(LC_MODEL_CAS_REGISTER, 0, 1, off, h, enc);
+    lc::encode(counter ? LC_MODEL_COUNTER : LC_MODEL_CAS_REGISTER, 0, 1, off, h, enc);
     long inword = 0;
     double work = 0;
     uint64_t live = 0;
     for (int64_t g = enc.step_off[0]; g < enc.step_off[1]; ++g) {
       if (g > enc.step_off[0]) live &= ~(1ull << enc.step_slot[g - 1]);
       for (int64_t q = enc.inv_off[g]; q < enc.inv_off[g + 1]; ++q) live |= 1ull << enc.inv_slot[q];
-      inword += enc.step_slot[g] < 3;
+      inword += enc.step_slot[g] < n_iw;
       work += (double)(1ull << (64 - __builtin_clzll(live | 1)));
     }
     std::printf("%d %d %ld %ld %.0f\n", it, enc.err[0] ? -1 : enc.live_max[0], inword,

@@ -14,7 +14,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
-def test_slot_policy_keeps_widths(tmp_path):
+@pytest.mark.parametrize("model", ["register", "counter"])
+def test_slot_policy_keeps_widths(tmp_path, model):
+    """register: in-word slots 0..2 (8 masks x 8 states per word); counter: 0..5 (64 masks)."""
     exe = tmp_path / "slots"
     subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe),
                     os.path.join(ROOT, "tests", "sanitize", "slots_main.cpp"),
@@ -25,7 +27,8 @@ def test_slot_policy_keeps_widths(tmp_path):
         env.pop("LC_SLOTS", None)
         if pol == "lff":
             env["LC_SLOTS"] = "lff"
-        out = subprocess.run([str(exe)], capture_output=True, text=True, check=True, env=env, timeout=120).stdout
+        out = subprocess.run([str(exe), model], capture_output=True, text=True, check=True, env=env,
+                             timeout=120).stdout
         runs[pol] = [tuple(float(x) for x in line.split()) for line in out.splitlines()]
     a, b = runs["policy"], runs["lff"]
     assert len(a) == len(b) == 400
