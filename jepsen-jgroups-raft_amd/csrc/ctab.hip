@@ -180,48 +180,38 @@ __device__ __forceinline__ uint64_t ct_x(const uint64_t* B, uint32_t w, uint32_t
 }
 
 // One step's closure of word w (its frontier X): the hi pulls and the in-word closure. Returns R.
-// Every LDS load that depends on w alone (the hi sums, the pulled words, their EQ bases) is
-// issued before any is used, then every EQ lookup (pulls and in-word gates) at once: a word's
-// chain is three LDS round trips (word list -> loads -> EQ) plus the VALU closure.
-constexpr int CT_PB = 4;  // pulls per batch (a word of popcount q <= CT_PB: one batch)
 __device__ __forceinline__ uint64_t ct_word(const uint64_t* Bt, uint32_t w, const CStep* st, uint32_t live, int j,
                                             uint64_t X) {
+  const int s_hi = (int)st->sh[0][w & 127u] + (int)st->sh[1][(w >> 7) & 127u];
   const bool jhi = j >= CTAB_LO;
   const uint32_t jh = jhi ? 1u << (j - CTAB_LO) : 0u;
-  const bool holds_j = (w & jh) != 0;
-  uint32_t m = holds_j ? jh : w;
-  const int sh0 = st->sh[0][w & 127u], sh1 = st->sh[1][(w >> 7) & 127u];
-  int32_t cl[CTAB_LO];
-#pragma unroll
-  for (int k = 0; k < CTAB_LO; ++k) cl[k] = st->cq[k];  // (wave-uniform: the step's in-word ops)
+  uint32_t m = (w & jh) ? jh : w;
   uint64_t R = 0;
-  int s_hi = 0;
-  bool first = true;
-  do {  // the word's set hi bits, CT_PB at a time
-    int b[CT_PB];
-    uint64_t v[CT_PB];
-    int32_t c[CT_PB];
+  while (m) {  // the word's set hi bits, two at a time (their loads issued together; r4b A/B: a batch
+               // of four with every EQ lookup issued at once was 3 % slower on C2c)
+    int b[2];
+    uint64_t v[2];
+    int32_t c[2];
 #pragma unroll
-    for (int u = 0; u < CT_PB; ++u) {
+    for (int u = 0; u < 2; ++u) {
       b[u] = m ? __builtin_ctz(m) : -1;
       m &= m - 1;
     }
 #pragma unroll
-    for (int u = 0; u < CT_PB; ++u) {
+    for (int u = 0; u < 2; ++u) {
       v[u] = b[u] >= 0 ? Bt[w ^ (1u << b[u])] : 0ull;
       c[u] = b[u] >= 0 ? st->cq[CTAB_LO + b[u]] : CQ_NEVER;
     }
-    if (first) s_hi = sh0 + sh1, first = false;
 #pragma unroll
-    for (int u = 0; u < CT_PB; ++u) R |= v[u] & gate(st, c[u], s_hi);
-  } while (m);
-  if (holds_j) return R;  // a word holding j (hi) is produced by linearizing j last only
+    for (int u = 0; u < 2; ++u) R |= v[u] & gate(st, c[u], s_hi);
+  }
+  if (w & jh) return R;  // a word holding j (hi) is produced by linearizing j last only
   const uint64_t notj = jhi ? ~0ull : keep6(j);
   R &= notj;
   const uint32_t lo = live & 63u & ~(jhi ? 0u : 1u << j);
   uint64_t G[CTAB_LO];
 #pragma unroll
-  for (int k = 0; k < CTAB_LO; ++k) G[k] = ((live >> k) & 1u) ? gate(st, cl[k], s_hi) & keep6(k) & notj : 0ull;
+  for (int k = 0; k < CTAB_LO; ++k) G[k] = ((live >> k) & 1u) ? gate(st, st->cq[k], s_hi) & keep6(k) & notj : 0ull;
   for (;;) {  // the in-word closure: gated transfers until nothing changes
     const uint64_t R0 = R;
 #pragma unroll

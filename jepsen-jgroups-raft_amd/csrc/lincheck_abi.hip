@@ -2536,7 +2536,8 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
   // per-config :last-op; its grid-kernel re-run can take minutes at these widths (the crash
   // ramp's width-27 history did not finish in 3), so the report stops here unless asked
   // (LC_WIDE_CONFIGS=1). The verdict, failing op and explored count stand.
-  if (p->enc.live_max[0] > DENSE_WIDE_LMAX && p->enc.model == LC_MODEL_CAS_REGISTER &&
+  if (p->enc.live_max[0] > DENSE_WIDE_LMAX && p->enc.live_max[0] <= WIDE_LMAX &&
+      p->enc.model == LC_MODEL_CAS_REGISTER &&
       !(getenv("LC_WIDE_CONFIGS") && atoi(getenv("LC_WIDE_CONFIGS")) != 0)) {
     set_err(err, err_len, "failure configs unavailable: %d live slots (> %d: decided on the HBM tables)",
             p->enc.live_max[0], DENSE_WIDE_LMAX);
