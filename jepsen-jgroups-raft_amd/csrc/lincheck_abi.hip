@@ -586,16 +586,16 @@ struct lc_plan {
     nst[h] = 0;
     lm[h] = 0;
     bool ok = !v.err && v.n_states <= DENSE_MAX_STATES;
-    for (int64_t t = 0; t < v.n_steps && ok; ++t)  // a step's words must fit the decoders' window
-      if (v.step_ninv[t] > DENSE_MAX_NINV) ok = false;
+    int64_t max_ninv = 0;  // a step's words must fit the decoders' window
+    for (int64_t t = 0; t < v.n_steps; ++t) max_ninv = std::max(max_ninv, v.step_ninv[t]);
     // wider than the LDS tile teams can hold (or from LC_WIDE_MINW on, tests): tables in HBM.
     // (LC_DENSE_MAXW below 24 sends the widths between it and 25 to the grid kernel, as before.)
     const int wmin = wide_minw > 0 ? wide_minw : DENSE_WIDE_LMAX + 1;
-    if (ok && v.live_max >= wmin && v.live_max <= wide_maxw) {
+    if (ok && max_ninv <= WIDE_MAX_NINV && v.live_max >= wmin && v.live_max <= wide_maxw) {
       wide_sink(h, v);
       return false;  // (its invocation arrays stay: lc_failure_configs re-runs it on the grid kernel)
     }
-    ok = ok && v.live_max <= dense_maxw;
+    ok = ok && max_ninv <= DENSE_MAX_NINV && v.live_max <= dense_maxw;
     dense_ok[h] = ok;
     if (!ok) return false;
     nst[h] = (int32_t)v.n_steps;

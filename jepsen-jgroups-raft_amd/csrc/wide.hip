@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
         const uint64_t live = (uint64_t)(uint32_t)__shfl((int)wd, 0, 64) |
                               ((uint64_t)(uint32_t)__shfl((int)wd, 1, 64) << 31);
         const uint32_t j = (uint32_t)__shfl((int)wd, 2, 64);
-        const unsigned long long ob = __ballot(lane >= 3 && lane < 3 + DENSE_MAX_NINV && (wd & DENSE_OPW));
+        const unsigned long long ob = __ballot(lane >= 3 && lane < 3 + WIDE_MAX_NINV && (wd & DENSE_OPW));
         const int ninv = (int)__builtin_ctzll(~(ob >> 3));
         if (lane >= 3 && lane < 3 + ninv) sOps[wd & 63u] = decode_op((wd >> 8) & 0xffu, (wd >> 16) & 0xffu);
         // (after the stores: one wave's LDS ops stay in order)
@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
       const uint64_t live = (uint64_t)(uint32_t)__shfl((int)wd, 0, 64) |
                             ((uint64_t)(uint32_t)__shfl((int)wd, 1, 64) << 31);
       const uint32_t j = (uint32_t)__shfl((int)wd, 2, 64);
-      const unsigned long long ob = __ballot(lane >= 3 && lane < 3 + DENSE_MAX_NINV && (wd & DENSE_OPW));
+      const unsigned long long ob = __ballot(lane >= 3 && lane < 3 + WIDE_MAX_NINV && (wd & DENSE_OPW));
       const int ninv = (int)__builtin_ctzll(~(ob >> 3));
       const uint64_t plive = prev ? prev->live : 0ull;
       const int pj = prev ? (int)prev->j : -1;

@@ -17,6 +17,8 @@ namespace lc {
 constexpr int WIDE_LMAX = 35;       // widest history: 2 tables of 2^32 words (64 GiB of the 288 GB HBM)
 constexpr int WIDE_NOPIPE_LMAX = 31;  // the one-step-at-a-time kernel's layer prefix tables stop here
 constexpr int WIDE_OPS = 36;        // op-table entries per step (slots 0..34, + the pull loop's reads)
+constexpr int WIDE_MAX_NINV = 60;   // invocations per step (3 header words + 60 in a 64-lane read;
+                                    // never binding: a step's invocations are live, <= WIDE_LMAX)
 constexpr int WIDE_LOW_BITS = 19;   // a layer's words = high part x low part from the sorted list
 
 // Step stream of a wide history (host-built, its own buffer):
