@@ -1246,26 +1246,6 @@ constexpr int PIPE_XCD = 16384;  // XCD-compact workgroup roles in the big kerne
 constexpr int PIPE_CPRE = 65536;
 constexpr int PIPE_CW16 = 131072;  // tile teams: a credit window of 16 super-layers (else 8)
 constexpr int PIPE_WSPREAD = 262144;  // big kernel: WAVE histories one per workgroup (big_wave_mode)
-// LC_PIPE bit 19 (r4): a tile team's step after a team-slot return reads its frontier X from
-// another tile's mirror (tile r | jp, written by the previous step two super-layers earlier); each
-// wave loads the X words of its NEXT super-layer's words at the end of this one (the layout of
-// super-layer s + 1 is known at the end of s from the ring view and the start decision), so the
-// HBM round trip leaves the super-layer's critical path. Tagged mirrors only (the tag check makes
-// an early read safe: a word not yet written is polled); a prefetched value is used only when its
-// (step, word) matches the word the wave then takes.
-constexpr int PIPE_XPRE = 524288;
-// LC_PIPE bit 20 (r4): tagged tile teams end a super-layer with an LDS-only barrier (a release /
-// acquire fence on the local address space around s_barrier): the LDS tables and the ring are
-// all a super-layer hands to the next within a workgroup, the mirror words travel with their
-// tags, so the barrier need not wait for this super-layer's mirror stores (s_waitcnt vmcnt(0))
-// nor for loads already issued for the next one (PIPE_XPRE)
-constexpr int PIPE_LBAR = 1048576;
-
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 __device__ __forceinline__ bool poll_until(const DenseParams& p, const unsigned long long* f,
                                            unsigned long long need, uint64_t t0, long& spins) {
@@ -1350,11 +1330,6 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
   // the window's lag of 2 x 16 plus a step's span of at most H + T + 1 <= 25)
   const int cw = (p.pipe & PIPE_CW16) ? 16 : 8;
   static_assert((1 << DENSE_TEAM_MAXB) <= 4 * 64, "credit pre-poll registers");
-  // PIPE_XPRE: X words loaded a super-layer ahead (the packed loop's first pass)
-  const bool xpre_on = (p.pipe & PIPE_XPRE) && tagged && !(p.pipe & PIPE_SERIAL_SEGS);
-  uint64_t xga = 0, xgb = 0;  // the two tagged granules, loaded without waiting (checked at use)
-  uint32_t xkey = ~0u;  // (step << 12 | word row) the value belongs to
-  const bool lbar = (p.pipe & PIPE_LBAR) && tagged;
   for (int s = 0; t_ret < ns; ++s) {
     unsigned long long tp = timed ? now() : 0;
     if (s >= cw && (s & (cw - 1)) == 0) {  // credit: nobody more than cw super-layers behind
@@ -1495,13 +1470,7 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         // expanded); a tile holding j takes only T_j of r \ j
         const bool pl = tile_j || !(jloc_hi && ((w >> (j - 3)) & 1u));
         if (tagged) {
-          if (fx && xs >= 0) {
-            const uint32_t key = ((uint32_t)t << 12) | r, tg = tag_of(t - 1);
-            if (xpre_on && f0 < 1024u && xkey == key && (uint32_t)(xga >> 32) == tg && (uint32_t)(xgb >> 32) == tg)
-              xv = (uint32_t)xga | (xgb << 32);
-            else
-              xv = TagTab::ld(mirror(xs, t - 1), mp + r, tg, p.abort);
-          }
+          if (fx && xs >= 0) xv = TagTab::ld(mirror(xs, t - 1), mp + r, tag_of(t - 1), p.abort);
 #pragma unroll
           for (int b = 0; b < TB; ++b)
             pv[b] = (pl && ((pmask >> b) & 1u)) ? TagTab::ld(mirror(rank ^ (1 << b), t), mo + r, tag_of(t), p.abort)
@@ -1655,60 +1624,9 @@ __device__ __forceinline__ void team_pipe(const DenseParams& p, uint64_t* B, con
         ++t_run;
       }
     }
-    if (xpre_on) {
-      // the packed layout of super-layer s + 1, from this super-layer's ring view (the steps
-      // still running then, the one started just now with start s + 1), and the X words this
-      // wave will take there from other tiles' mirrors
-      const int s1 = s + 1;
-      const int il = t_run - 1 - t_ret_old;  // the newest running step's lane
-      const int st_l = (lane == il && h1.w == (1 << 30)) ? s1 : h1.w;
-      const int pst_l = (lane == il && h1.w == (1 << 30)) ? rdl(h1.w, il > 0 ? il - 1 : 0) : h2.x;
-      const bool run1 = dec_l && lane >= lead && tl < t_run;
-      const int q1 = s1 - st_l - dr_l;
-      const bool seg1 = run1 && (rank & ~lteam_l) == 0 && q1 >= 0 && q1 <= h1.z;
-      int xs1 = -1;
-      uint32_t nq1 = 0, o1 = 0, mp1 = 0;
-      if (seg1) {
-        nq1 = binom[h1.z * BINOM_N + q1], o1 = wof[q1];
-        mp1 = cum[h2.y * BINOM_N + min(q1, h2.y)];
-        if (h1.y >= lb && !((uint32_t)rank & (h0.y >> lb))) xs1 = rank | (1 << (h1.y - lb));
-      }
-      (void)pst_l;
-      const uint64_t segm1 = __ballot(seg1);
-      uint32_t total1 = 0;
-      for (uint64_t m = segm1; m; m &= m - 1) total1 += (rdl(nq1, (int)__builtin_ctzll(m)) + 63u) & ~63u;
-      xkey = ~0u;
-      do {
-        const uint32_t f0 = (uint32_t)(tid & ~63);
-        if (f0 >= total1) break;
-        int i = 0;
-        uint32_t e = 0, acc = 0;
-        for (uint64_t m = segm1; m; m &= m - 1) {
-          const int k = (int)__builtin_ctzll(m);
-          if (f0 >= acc) i = k, e = acc;
-          acc += (rdl(nq1, k) + 63u) & ~63u;
-        }
-        const int xs = rdl(xs1, i);
-        if (xs < 0) break;
-        const uint32_t nq = rdl(nq1, i), r = f0 - e + (uint32_t)lane;
-        if (r >= nq) break;
-        const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i);
-        const uint32_t w = words[rdl(o1, i) + r];
-        if (w & ~((live & lmask) >> 3)) break;
-        const bool tile_fresh = ((uint32_t)rank & (fresh >> lb)) != 0;
-        if (tile_fresh || (w & ((fresh & lmask) >> 3))) break;
-        const int t = t_ret_old + i;
-        const uint64_t* slot = mirror(xs, t - 1);
-        const uint32_t wi = rdl(mp1, i) + r;
-        xga = HbmTab::ld(&slot[2 * wi]);  // (issued now, waited for where they are used)
-        xgb = HbmTab::ld(&slot[2 * wi + 1]);
-        xkey = ((uint32_t)t << 12) | r;
-      } while (false);
-    }
     if (timed) ph[1] += now() - tp, tp = now();
     if (wide_any && !tagged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-    if (lbar) lds_barrier();
-    else __syncthreads();
+    __syncthreads();
     if (tid == 0) st_agent(&flags[rank], (unsigned long long)(s + 1));
     if (timed) ph[2] += now() - tp, ph[5] += 1;
   }

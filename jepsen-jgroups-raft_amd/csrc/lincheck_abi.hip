@@ -177,7 +177,8 @@ struct lc_plan {
   DevArray d_wtab, d_wstream, d_wmeta, d_wres, d_wbar;
   int wide_maxw = WIDE_LMAX, wide_minw = 0;  // LC_WIDE_MAXW (0: off) / LC_WIDE_MINW (tests)
   int wide_grid = 0;  // LC_WIDE_GRID: at most this many workgroups for the HBM tables (0: one per CU)
-  int wide_watchdog_ms = 20000;  // LC_WIDE_WATCHDOG_MS: a grid barrier's longest wait (tests force it low)
+  int wide_watchdog_ms = 20000;  // LC_WIDE_WATCHDOG_MS: a grid barrier's longest wait
+  bool wide_force_abort = false;  // LC_WIDE_FORCE_ABORT=1 (tests): the abort word set before launch
   bool wide_pipe = true;  // LC_WIDE_PIPE=0: one step at a time (a grid barrier per popcount layer)
   // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
   // begin / step count / table width, and the queue order
@@ -372,6 +373,7 @@ struct lc_plan {
     if ((e = getenv("LC_WIDE_PIPE"))) wide_pipe = atoi(e) != 0;
     if ((e = getenv("LC_WIDE_GRID"))) wide_grid = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_WATCHDOG_MS")) && atoi(e) >= 0) wide_watchdog_ms = atoi(e);
+    if ((e = getenv("LC_WIDE_FORCE_ABORT"))) wide_force_abort = atoi(e) != 0;
     if ((e = getenv("LC_CTAB_MAXW"))) ctab_maxw = std::max(0, std::min(atoi(e), CTAB_LMAX));
     if ((e = getenv("LC_CTAB_PIPE"))) ctab_pipe = atoi(e);
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
@@ -410,7 +412,7 @@ struct lc_plan {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
-    ctab_maxw = CTAB_LMAX, ctab_pipe = 1, wide_watchdog_ms = 20000;
+    ctab_maxw = CTAB_LMAX, ctab_pipe = 1, wide_watchdog_ms = 20000, wide_force_abort = false;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.2, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 12, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, rot_chain_min = 14, batch_hist = 600, mid_maxw = 0;
@@ -1830,6 +1832,10 @@ struct lc_plan {
     HIP_TRY(d_wbar.ensure(wide_bar_bytes() + 8));
     HIP_TRY(hipMemsetAsync(d_wres.p, 0, r_bytes, stream));
     HIP_TRY(hipMemsetAsync(d_wbar.p, 0, wide_bar_bytes() + 8, stream));
+    if (wide_force_abort) {  // (tests: the path a fired watchdog takes, without waiting 20 s for one)
+      static const int32_t one = 1;
+      HIP_TRY(hipMemcpyAsync((char*)d_wbar.p + wide_bar_bytes(), &one, 4, hipMemcpyHostToDevice, stream));
+    }
     WideParams p{};
     p.n = nwd;
     p.sbeg = (const int64_t*)d_wmeta.p;

@@ -103,17 +103,6 @@ def test_gpu_c2_full_size_vs_oracle():
     _cmp(g, oracle.check_one("cas-register", h), 0, "c2-full")
 
 
-@pytest.mark.parametrize("bits", [524288, 1048576, 524288 | 1048576], ids=["xpre", "lbar", "xpre-lbar"])
-def test_gpu_c2_full_size_x_prefetch(bits, monkeypatch):
-    """C2 at full size with LC_PIPE bits 19/20 (r4): a tile team's X words of the next
-    super-layer issued from other tiles' mirrors at the end of the current one (checked by
-    their tags where used), and the super-layer's LDS-only barrier; bit-exact with the oracle."""
-    monkeypatch.setenv("LC_PIPE", str(217039 | bits))
-    h = synth.gen_config("c2")
-    g = _lib.check(1, 0, h)
-    _cmp(g, oracle.check_one("cas-register", h), 0, f"c2-pipe-{bits}")
-
-
 # C4 (BASELINE configs[3]): one 100k-op history with crashed :info ops. Its full-size oracle
 # verdict and explored count (tests/golden/c4_oracle.json: the C oracle on one thread, 3.0 h,
 # made by tests/golden/pin_c4.py) are the fixture every GPU path must reproduce.
@@ -713,8 +702,8 @@ def test_gpu_dense_tile_teams_small_tiles(lbits, monkeypatch):
     p.close()
 
 
-@pytest.mark.parametrize("pipe", ["207", "463", "719", "975", "525263", "1573839"],
-                         ids=["tokens", "tagged", "tokens-dbl", "tagged-dbl", "tagged-dbl-xpre", "tagged-dbl-xpre-lbar"])
+@pytest.mark.parametrize("pipe", ["207", "463", "719", "975"],
+                         ids=["tokens", "tagged", "tokens-dbl", "tagged-dbl"])
 @pytest.mark.parametrize("rot,lbits", [("1", "14"), ("3", "13"), ("9", "15"), ("9", None)])
 def test_gpu_dense_tile_teams_rotated(rot, lbits, pipe, monkeypatch):
     """LC_TEAM_ROT: a tile team's lowest slots relabelled as its team bits (every tile holds a
@@ -1183,11 +1172,12 @@ def test_gpu_wide_tables_past_31_slots():
 
 
 def test_gpu_wide_watchdog_abort_is_unknown(monkeypatch):
-    """when the HBM tables' grid barrier watchdog fires (forced here with
-    LC_WIDE_WATCHDOG_MS=0) the call still succeeds: the wide histories it did not finish are
-    :unknown with LC_H_ABORTED, every other history of the call keeps its answer."""
+    """when the HBM tables' grid barrier watchdog fires (its abort word forced here
+    with LC_WIDE_FORCE_ABORT=1, as a fired watchdog leaves it) the call still succeeds: the wide
+    histories it did not finish are :unknown with LC_H_ABORTED, every other history of the call
+    keeps its answer."""
     monkeypatch.setenv("LC_WIDE_MINW", "12")
-    monkeypatch.setenv("LC_WIDE_WATCHDOG_MS", "0")
+    monkeypatch.setenv("LC_WIDE_FORCE_ABORT", "1")
     narrow = [synth.gen_register(200, 4, 0.01, 56000 + t, invalid=(t % 2 == 1)) for t in range(6)]
     wide = synth.gen_register(400, 16, 0.01, 56100, n_crashed=2)
     h = H.concat(narrow + [wide])
@@ -1199,7 +1189,7 @@ def test_gpu_wide_watchdog_abort_is_unknown(monkeypatch):
     exp = oracle.check_many("cas-register", h.select(list(range(len(narrow)))))
     for k in range(len(narrow)):
         _cmp(g, exp[k], k, "beside an aborted wide history")
-    monkeypatch.delenv("LC_WIDE_WATCHDOG_MS")
+    monkeypatch.delenv("LC_WIDE_FORCE_ABORT")
     g2 = _lib.check(1, 0, h)  # the next call runs normally
     assert int(g2["valid"][last]) == oracle.check_one("cas-register", h.select([last]))["valid"]
 
