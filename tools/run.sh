@@ -25,7 +25,10 @@ for step in "$@"; do
   echo "[run.sh] $(date +%T) $step" | tee -a "$out/steps.log"
   case $kind in
     test)
-      timeout -k 10 1000 python -u -m pytest $(sp "$rest") -x -v --timeout 300 --timeout-method thread \
+      # (commas separate arguments; '@' stands for a space inside one, e.g. -k,fuzz@or@wide)
+      IFS=',' read -ra A <<< "$rest"
+      for i in "${!A[@]}"; do A[$i]=${A[$i]//@/ }; done
+      timeout -k 10 1000 python -u -m pytest "${A[@]}" -x -v --timeout 300 --timeout-method thread \
         > "$out/pytest_$(echo "$rest" | tr -c 'A-Za-z0-9_' _ | cut -c1-40).log" 2>&1 || { echo "[run.sh] FAILED $step"; exit 1; } ;;
     bench)
       name=${rest%%:*}; args=$(sp "${rest#*:}")
