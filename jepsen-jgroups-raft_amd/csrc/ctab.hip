@@ -32,7 +32,7 @@
 namespace lc {
 namespace {
 
-constexpr int CT_TEAM = 1024;
+constexpr int CT_TEAM = 1024;  // (r4i: 512 threads, two passes per super-layer, 30.7 -> 41.4 ms on C2c)
 constexpr int CT_RING = 16;
 constexpr int CT_CAPW = 1 << (CTAB_LMAX - CTAB_LO);  // LDS table words (128 KiB)
 constexpr int CT_BINOM = 24;
@@ -180,9 +180,25 @@ __device__ __forceinline__ uint64_t ct_x(const uint64_t* B, uint32_t w, uint32_t
 }
 
 // One step's closure of word w (its frontier X): the hi pulls and the in-word closure. Returns R.
+// pf (builds with LC_CT_WORDPROF and LC_DEBUG, else null): cycles to the hi sums, the pulls, the
+// gates, the closure; closure sweeps. (Compiled out by default: the checks alone cost C2c 3 %.)
 __device__ __forceinline__ uint64_t ct_word(const uint64_t* Bt, uint32_t w, const CStep* st, uint32_t live, int j,
-                                            uint64_t X) {
+                                            uint64_t X, unsigned long long* pf = nullptr) {
+#ifdef LC_CT_WORDPROF
+  unsigned long long tp = pf ? __builtin_amdgcn_s_memtime() : 0;
+  auto pmark = [&](int k) {
+    if (pf) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const unsigned long long tn = __builtin_amdgcn_s_memtime();
+      pf[k] += tn - tp;
+      tp = tn;
+    }
+  };
+#else
+  auto pmark = [](int) {};
+#endif
   const int s_hi = (int)st->sh[0][w & 127u] + (int)st->sh[1][(w >> 7) & 127u];
+  pmark(0);
   const bool jhi = j >= CTAB_LO;
   const uint32_t jh = jhi ? 1u << (j - CTAB_LO) : 0u;
   uint32_t m = (w & jh) ? jh : w;
@@ -205,20 +221,43 @@ __device__ __forceinline__ uint64_t ct_word(const uint64_t* Bt, uint32_t w, cons
 #pragma unroll
     for (int u = 0; u < 2; ++u) R |= v[u] & gate(st, c[u], s_hi);
   }
+  pmark(1);
   if (w & jh) return R;  // a word holding j (hi) is produced by linearizing j last only
   const uint64_t notj = jhi ? ~0ull : keep6(j);
   R &= notj;
   const uint32_t lo = live & 63u & ~(jhi ? 0u : 1u << j);
   uint64_t G[CTAB_LO];
+#ifdef LC_CT_GATES_BATCH
+  {  // the low slots' EQ bases (one broadcast read each), then their six EQ words, all issued at once
+    int32_t cl[CTAB_LO];
+    uint64_t el[CTAB_LO];
+#pragma unroll
+    for (int k = 0; k < CTAB_LO; ++k) cl[k] = st->cq[k];
+#pragma unroll
+    for (int k = 0; k < CTAB_LO; ++k) el[k] = st->eq[(uint32_t)(cl[k] - s_hi) & 63u];
+#pragma unroll
+    for (int k = 0; k < CTAB_LO; ++k) {
+      const uint32_t i = (uint32_t)(cl[k] - s_hi);
+      const uint64_t g = cl[k] == CQ_UNC ? ~0ull : i < 64u ? el[k] : 0ull;
+      G[k] = ((live >> k) & 1u) ? g & keep6(k) & notj : 0ull;
+    }
+  }
+#else
 #pragma unroll
   for (int k = 0; k < CTAB_LO; ++k) G[k] = ((live >> k) & 1u) ? gate(st, st->cq[k], s_hi) & keep6(k) & notj : 0ull;
+#endif
+  pmark(2);
   for (;;) {  // the in-word closure: gated transfers until nothing changes
     const uint64_t R0 = R;
 #pragma unroll
     for (int k = 0; k < CTAB_LO; ++k)
       if ((lo >> k) & 1u) R |= ((X | R) & G[k]) << (1 << k);
+#ifdef LC_CT_WORDPROF
+    if (pf) pf[4] += 1;
+#endif
     if (R == R0) break;
   }
+  pmark(3);
   if (!jhi) {  // the returning op, linearized last
 #pragma unroll
     for (int k = 0; k < CTAB_LO; ++k)
@@ -309,9 +348,10 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
     unsigned long long expl = 0;
     int fail_t = -1;
     int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0;  // decoded, started, retired
-    // LC_DEBUG: super-layer phase cycles of wave 0 and of the decoder wave (s_memtime)
-    const bool prof = p.prof != nullptr && (tt == 0 || tt == CT_TEAM - 64);
-    unsigned long long ph[4] = {0, 0, 0, 0}, tp = prof ? __builtin_amdgcn_s_memtime() : 0, nsl = 0;
+    // LC_DEBUG: super-layer phase cycles of every wave (s_memtime) and the words it closed
+    const bool prof = p.prof != nullptr;
+    unsigned long long ph[4] = {0, 0, 0, 0}, tp = prof ? __builtin_amdgcn_s_memtime() : 0, nsl = 0, nwd = 0;
+    unsigned long long pw[6] = {0, 0, 0, 0, 0, 0};  // a word's phases (ct_word's pf), + to the word
     auto mark = [&](int k) {
       if (prof) {
         const unsigned long long tnow = __builtin_amdgcn_s_memtime();
@@ -357,6 +397,9 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
       uint32_t total = 0;
       for (uint64_t m = segm; m; m &= m - 1) total += (rdl(nq_l, (int)__builtin_ctzll(m)) + 63u) & ~63u;
       for (uint32_t f0 = (uint32_t)(tt & ~63); f0 < total; f0 += (uint32_t)CT_TEAM) {
+#ifdef LC_CT_WORDPROF
+        const unsigned long long tpw = prof ? __builtin_amdgcn_s_memtime() : 0;
+#endif
         int i = 0;
         uint32_t e = 0, acc = 0;
         for (uint64_t m = segm; m; m &= m - 1) {
@@ -373,12 +416,26 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
         if (w & ~(live >> CTAB_LO)) continue;
         CStep* st = &sRing[t % CT_RING];
         uint64_t* const Bt = tab(t);
+#ifdef LC_CT_WORDPROF
+        if (prof) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const unsigned long long tn = __builtin_amdgcn_s_memtime();
+          pw[5] += tn - tpw;  // to the word (segment lookup, word index, X)
+        }
+#endif
         const uint64_t X = ct_x(tab(t - 1), w, fresh >> CTAB_LO, jp, st->keep_lo);
+        // (r4k: wave-uniform control flow in the word, every lane through every pull round and
+        // closure sweep with masked loads, was 8 % slower on C2c4: the divergent form is kept)
+        #ifdef LC_CT_WORDPROF
+        const uint64_t R = ct_word(Bt, w, st, live, j, X, prof ? pw : nullptr);
+#else
         const uint64_t R = ct_word(Bt, w, st, live, j, X);
+#endif
         Bt[w] = X | R;
         expl += (uint32_t)__popcll(R);
         if (t > 0) st_fout += (uint32_t)__popcll(X);
         if (X) st->anyx = 1;
+        if (prof) ++nwd;
       }
       mark(1);
       // ---- decode ahead into a slot nobody read in this super-layer
@@ -410,9 +467,20 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
       mark(3);
     }
     if (prof) {
-      unsigned long long* q = p.prof + (tt == 0 ? 0 : 5);
-      for (int k = 0; k < 4; ++k) atomicAdd(&q[k], ph[k]);
-      atomicAdd(&q[4], nsl);
+      for (int off = 32; off > 0; off >>= 1) nwd += __shfl_down(nwd, off, 64);
+      if (lane == 0) {
+        unsigned long long* q = p.prof + 8 * (tt >> 6);
+        for (int k = 0; k < 4; ++k) atomicAdd(&q[k], ph[k]);
+        atomicAdd(&q[4], nsl);
+        atomicAdd(&q[5], nwd);
+        atomicAdd(&q[6], pw[0] + pw[1]);  // hi sums + pulls
+        atomicAdd(&q[7], pw[2]);          // gates
+        unsigned long long* r = p.prof + 128 + 4 * (tt >> 6);
+        atomicAdd(&r[0], pw[3]);  // closure
+        atomicAdd(&r[1], pw[5]);  // to the word
+        atomicAdd(&r[2], pw[4]);  // closure sweeps (lane 0's)
+        atomicAdd(&r[3], pw[1]);  // pulls alone
+      }
     }
     if (fail_t < 0 && ns > 0) {  // the last step's return
       const CStep* st = &sRing[(ns - 1) % CT_RING];

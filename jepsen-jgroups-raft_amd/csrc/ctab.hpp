@@ -53,7 +53,7 @@ struct CtabParams {
   unsigned long long* explored;  // [n_hist]
   unsigned long long* stats;     // [2] frontier configs out, steps
   unsigned long long* stamps;    // [n_hist][2] start, end (s_memrealtime, 100 MHz); may be null
-  unsigned long long* prof;      // LC_DEBUG [2 waves (0, decoder)][5]: super-layer phase cycles
+  unsigned long long* prof;      // LC_DEBUG [16 waves][8]: super-layer phase cycles, super-layers, words closed
                                  // (ring view, words, decode + start, barrier) and super-layers
   int32_t pipe;                  // bit 0: double-buffered tables when two fit (default on)
 };

@@ -130,6 +130,30 @@ __device__ __forceinline__ uint64_t pull_set(const uint64_t* B, uint32_t w, int 
   const uint32_t jh = j < 3 ? 0u : 1u << (j - 3);
   uint32_t m = (w & jh) ? jh : w;
   uint64_t R = 0;
+#ifdef LC_PULL_BF
+  // branch-free pairs: a lane without a second bit reads its own word and slot 3's op, masked after
+  while (m) {
+    int b[2];
+    uint64_t v[2];
+    OpSel o[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      b[u] = m ? __builtin_ctz(m) : -1;
+      m &= m - 1;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      v[u] = B[w ^ (b[u] >= 0 ? 1u << b[u] : 0u)];
+      o[u] = ops[(b[u] >= 0 ? b[u] : 0) + 3];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint64_t x = transfer(o[u], (foldm >> ((b[u] >= 0 ? b[u] : 0) + 3)) & 1u, v[u]);
+      R |= b[u] >= 0 ? x : 0ull;
+    }
+  }
+  return R;
+#endif
   while (m) {  // (a lane's trip count is ceil(popcount / 2); a layer's words share the popcount;
                // pairs, not quads: quads spill registers in the big kernel, r2h3: C3 11.5 vs 11.0 ms)
     int b[2];
@@ -636,7 +660,14 @@ struct __attribute__((aligned(16))) PipeStep {
   uint32_t live, fresh, foldm, anyx;
   int32_t j, jp, H, start;  // H: layers - 1 over the LOCAL slots (all slots outside tile teams)
   int32_t pstart, hp, pad0, pad1;  // tile teams: the previous step's start and H
+#ifndef LC_RING_NOPAD
+  // 272 B, not 256: a ring view's lanes read consecutive entries' headers (16 B each), which at a
+  // 256-B stride all fall into the same four LDS banks (a 16-way conflict per read); at 272 B
+  // (68 dwords) sixteen entries cover all 64 banks once
+  uint32_t bank_pad[4];
+#endif
 };
+static_assert(sizeof(PipeStep) % 16 == 0, "ring entries stay 16-B aligned (the pull batches' op pairs)");
 
 __device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 

@@ -1716,8 +1716,8 @@ struct lc_plan {
     HIP_TRY(hipMemsetAsync(d_dstamps.p, 0, (size_t)std::max(n, 1) * 32, stream));
     p.stamps = d_dstamps.as<unsigned long long>();
     if (debug()) {
-      HIP_TRY(d_dlhist.ensure(16 * 8));
-      HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, 16 * 8, stream));
+      HIP_TRY(d_dlhist.ensure(16 * 12 * 8));
+      HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, 16 * 12 * 8, stream));
       p.prof = d_dlhist.as<unsigned long long>();
     }
     const int grid = std::min(nc, dgrid_c);
@@ -1773,14 +1773,21 @@ struct lc_plan {
                   enc.n_steps(h), (T[2 * h + 1] - T[2 * h]) / 100.0,
                   (T[2 * h + 1] - T[2 * h]) / 100.0 / std::max(1, enc.n_steps(h)));
         }
-      unsigned long long P[10];
+      // per wave: ring, words, decode+start, barrier cycles, super-layers, words closed, then (LC_DEBUG
+      // word phases, serialised by their marks) hi sums + pulls, gates | closure, to the word, sweeps, pulls
+      unsigned long long P[16 * 12];
       if (hipMemcpy(P, d_dlhist.p, sizeof(P), hipMemcpyDeviceToHost) == hipSuccess)
-        for (int wv = 0; wv < 2; ++wv)
-          if (P[5 * wv + 4])
-            fprintf(stderr, "[lincheck]   %s: per super-layer cycles: ring %.0f words %.0f decode+start %.0f barrier %.0f "
-                    "(%llu super-layers)\n", wv ? "decoder wave" : "wave 0", P[5 * wv] / (double)P[5 * wv + 4],
-                    P[5 * wv + 1] / (double)P[5 * wv + 4], P[5 * wv + 2] / (double)P[5 * wv + 4],
-                    P[5 * wv + 3] / (double)P[5 * wv + 4], P[5 * wv + 4]);
+        for (int wv = 0; wv < 16; ++wv)
+          if (const unsigned long long *q = P + 8 * wv, *r = P + 128 + 4 * wv; q[4])
+            fprintf(stderr, "[lincheck]   wave %2d%s: per super-layer cycles: ring %.0f words %.0f decode+start %.0f "
+                    "barrier %.0f; %.1f words (%llu super-layers)%s\n", wv, wv == 15 ? " (decoder)" : "",
+                    q[0] / (double)q[4], q[1] / (double)q[4], q[2] / (double)q[4], q[3] / (double)q[4],
+                    q[5] / (double)q[4], q[4],
+                    r[1] ? ("; words phase (LC_CT_WORDPROF build): to-word " + std::to_string(r[1] / q[4]) + " sums " +
+                            std::to_string((q[6] - r[3]) / q[4]) + " pulls " + std::to_string(r[3] / q[4]) + " gates " +
+                            std::to_string(q[7] / q[4]) + " closure " + std::to_string(r[0] / q[4]))
+                               .c_str()
+                         : "");
     }
     return 0;
   }
@@ -1816,7 +1823,7 @@ struct lc_plan {
       dense_word_list(DENSE_WORD_BITS, wl.data());
       if ((rc = upload(d_dwords, wl))) return rc;
     }
-    // meta: sbeg | anyv_off | nsteps | lmax; results: explored | any | status | fail | stats[2] |
+    // meta: sbeg | anyv_off | nsteps | lmax; results: explored | any | status | fail | stats[4] |
     // the pipelined kernel's per-step bits
     std::vector<int64_t> aoff(nwd);
     int64_t abits = 0;
@@ -1827,7 +1834,7 @@ struct lc_plan {
     HIP_TRY(hipMemcpy((char*)d_wmeta.p + m_sb, aoff.data(), m_sb, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy((char*)d_wmeta.p + 2 * m_sb, nst.data(), m_ns, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy((char*)d_wmeta.p + 2 * m_sb + m_ns, lmx.data(), (size_t)nwd, hipMemcpyHostToDevice));
-    const size_t r_bytes = (size_t)nwd * 24 + 16 + (size_t)abits * 4;
+    const size_t r_bytes = (size_t)nwd * 24 + 32 + (size_t)abits * 4;
     HIP_TRY(d_wres.ensure(r_bytes));
     HIP_TRY(d_wbar.ensure(wide_bar_bytes() + 8));
     HIP_TRY(hipMemsetAsync(d_wres.p, 0, r_bytes, stream));
@@ -1854,7 +1861,7 @@ struct lc_plan {
     p.status = (int32_t*)(rex + 2 * nwd);
     p.fail_step = p.status + nwd;
     p.stats = (unsigned long long*)(p.fail_step + nwd);
-    p.anyv = (uint32_t*)(p.stats + 2);
+    p.anyv = (uint32_t*)(p.stats + 4);
     p.bar = d_wbar.as<unsigned>();
     p.abort = (int32_t*)((char*)d_wbar.p + wide_bar_bytes());
     p.watchdog = (uint64_t)wide_watchdog_ms * 100000ull;
@@ -1911,8 +1918,9 @@ struct lc_plan {
     }
     stats[33] += alg;
     if (debug())
-      fprintf(stderr, "[lincheck] wide: %d histories (tables of 2^%d words in HBM), %.3f ms, steps=%llu Fout=%llu\n",
-              nwd, std::max(0, lmax - 3), t, ss[1], ss[0]);
+      fprintf(stderr, "[lincheck] wide: %d histories (tables of 2^%d words in HBM), %.3f ms, steps=%llu Fout=%llu; "
+              "words visited %llu, stored nonzero %llu (%.2f %%)\n", nwd, std::max(0, lmax - 3), t, ss[1], ss[0], ss[2],
+              ss[3], 100.0 * (double)ss[3] / (double)std::max(1ull, ss[2]));
     ran = true;
     return 0;
   }

@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
     sLay[tid] = o;
   }
   const int64_t gtid = (int64_t)blockIdx.x * WWG + tid, gstride = (int64_t)gridDim.x * WWG;
-  unsigned long long st_fout = 0, st_steps = 0;
+  unsigned long long st_fout = 0, st_steps = 0, st_wv = 0, st_wnz = 0;
   for (int i = 0; i < p.n; ++i) {
     const int ns = p.nsteps[i];
     uint64_t* const T0 = p.tab;
@@ -214,6 +214,7 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
           expl += (uint64_t)__popcll(R);
           if (t > 0) st_fout += (uint64_t)__popcll(X);
           anyx |= X;
+          ++st_wv, st_wnz += (X | R) != 0;
         }
         if (q == H && __any(anyx != 0) && lane == 0)  // step t-1's post-return frontier held a config
           __hip_atomic_fetch_max(&p.any[i], (unsigned long long)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -263,9 +264,15 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
     // (the next history's first store is to T1[0]: every workgroup is past this one's reads)
     if (!wide_sync(p, &sAbort)) break;
   }
-  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
+  for (int off = 32; off > 0; off >>= 1) {
+    st_fout += __shfl_down(st_fout, off, 64);
+    st_wv += __shfl_down(st_wv, off, 64);
+    st_wnz += __shfl_down(st_wnz, off, 64);
+  }
   if (lane == 0 && st_fout) atomicAdd(&p.stats[0], st_fout);
   if (blockIdx.x == 0 && tid == 0 && st_steps) atomicAdd(&p.stats[1], st_steps);
+  if (lane == 0 && st_wv) atomicAdd(&p.stats[2], st_wv);
+  if (lane == 0 && st_wnz) atomicAdd(&p.stats[3], st_wnz);
 }
 
 // ---- pipelined steps (WideParams.pipe): the schedule of dense.hip's history_pipe with the whole
@@ -313,7 +320,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
     sLay[tid] = o;
   }
   const int64_t gtid = (int64_t)blockIdx.x * WWG + tid, gstride = (int64_t)gridDim.x * WWG;
-  unsigned long long st_fout = 0, st_steps = 0;
+  unsigned long long st_fout = 0, st_steps = 0, st_wv = 0, st_wnz = 0;
   for (int i = 0; i < p.n && !sAbort; ++i) {
     const int ns = p.nsteps[i];
     uint64_t* const T0 = p.tab;
@@ -420,6 +427,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
         expl += (uint64_t)__popcll(R);
         if (t > 0) st_fout += (uint64_t)__popcll(X);
         if (X) anyseg |= 1u << si;
+        ++st_wv, st_wnz += (X | R) != 0;
       }
       // the steps this wave saw a config in: one atomic OR per step per wave
       for (int si = 0; si < t_run - t_ret; ++si)
@@ -486,9 +494,15 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
     }
     if (!wide_sync(p, &sAbort)) break;
   }
-  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
+  for (int off = 32; off > 0; off >>= 1) {
+    st_fout += __shfl_down(st_fout, off, 64);
+    st_wv += __shfl_down(st_wv, off, 64);
+    st_wnz += __shfl_down(st_wnz, off, 64);
+  }
   if (lane == 0 && st_fout) atomicAdd(&p.stats[0], st_fout);
   if (blockIdx.x == 0 && tid == 0 && st_steps) atomicAdd(&p.stats[1], st_steps);
+  if (lane == 0 && st_wv) atomicAdd(&p.stats[2], st_wv);
+  if (lane == 0 && st_wnz) atomicAdd(&p.stats[3], st_wnz);
 }
 
 }  // namespace

@@ -43,7 +43,7 @@ struct WideParams {
   unsigned long long* any;    // [n] latest step (+1) whose frontier held a config (zeroed)
   unsigned* bar;              // grid barrier words (zeroed before launch)
   int32_t* abort;             // a barrier watchdog fired
-  unsigned long long* stats;  // [2] frontier-out configs, steps
+  unsigned long long* stats;  // [4] frontier-out configs, steps, words visited, words stored nonzero
   int32_t pipe;               // 1: pipelined steps (wide_pipe_kernel), 0: one step at a time
   uint32_t* anyv;             // pipelined: per history, bit t = some X of step t was nonzero (zeroed)
   uint64_t watchdog;          // s_memrealtime ticks (100 MHz) a grid barrier may wait before *abort
