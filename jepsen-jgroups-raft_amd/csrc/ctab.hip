@@ -39,6 +39,7 @@ constexpr int CT_BINOM = 24;
 constexpr int32_t CQ_UNC = 0x3fffffff;   // cq sentinel: the op steps from any config
 constexpr int32_t CQ_NEVER = -0x3fffffff;  // ... from none (out of the EQ range whatever the sum)
 constexpr int CT_PIPE_DBL = 1;
+constexpr int CT_PIPE_DYN = 2;  // LC_CTAB_PIPE bit 1: multi-pass super-layers' chunks from an LDS counter
 
 struct __attribute__((aligned(16))) CStep {
   uint32_t live, fresh, anyx;
@@ -286,6 +287,7 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
   __shared__ uint32_t sWOff[CT_BINOM + 2];
   __shared__ int sQ;
   __shared__ unsigned long long sExpl;
+  __shared__ uint32_t sChunk[2];  // CT_PIPE_DYN: the super-layers' chunk counters (by parity)
   const int tt = threadIdx.x, lane = tt & 63;
   const bool decoder = tt >= CT_TEAM - 64;  // the last wave: packed passes fill the low threads first
   init_binom(sBinom, tt, CT_TEAM);
@@ -338,6 +340,7 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
     }
     __syncthreads();
     if (tt == 0) B2[0] = 1;  // the initial config: nothing linearized (step 0 reads tab(-1))
+    if (tt < 2) sChunk[tt] = 0u;
     StreamWin sw;
     int64_t pos = p.sbeg[h];
     if (ns > 0 && decoder) {
@@ -396,7 +399,21 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
       // on a single step: its parameters are wave-uniform)
       uint32_t total = 0;
       for (uint64_t m = segm; m; m &= m - 1) total += (rdl(nq_l, (int)__builtin_ctzll(m)) + 63u) & ~63u;
-      for (uint32_t f0 = (uint32_t)(tt & ~63); f0 < total; f0 += (uint32_t)CT_TEAM) {
+      // CT_PIPE_DYN: a super-layer of more words than threads hands its 64-word chunks out from an
+      // LDS counter (the next chunk fetched while this one runs), so the waves that lose issue
+      // arbitration under load take fewer chunks instead of ending the super-layer last
+      const bool dyn = (p.pipe & CT_PIPE_DYN) && total > (uint32_t)CT_TEAM;
+      if (tt == 0) sChunk[(s + 1) & 1] = 0u;  // the next super-layer's counter (unused in this one)
+      auto fetch = [&]() -> uint32_t {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(&sChunk[s & 1], 1u);
+        return 64u * (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+      };
+      uint32_t f0 = dyn ? fetch() : (uint32_t)(tt & ~63);
+      for (; f0 < total;) {
+        const uint32_t f_next = dyn ? fetch() : f0 + (uint32_t)CT_TEAM;
+        const uint32_t f_this = f0;
+        f0 = f_next;
 #ifdef LC_CT_WORDPROF
         const unsigned long long tpw = prof ? __builtin_amdgcn_s_memtime() : 0;
 #endif
@@ -404,10 +421,10 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
         uint32_t e = 0, acc = 0;
         for (uint64_t m = segm; m; m &= m - 1) {
           const int k = (int)__builtin_ctzll(m);
-          if (f0 >= acc) i = k, e = acc;
+          if (f_this >= acc) i = k, e = acc;
           acc += (rdl(nq_l, k) + 63u) & ~63u;
         }
-        const uint32_t nq = rdl(nq_l, i), r = f0 - e + (uint32_t)lane;
+        const uint32_t nq = rdl(nq_l, i), r = f_this - e + (uint32_t)lane;
         const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i);
         const int j = rdl(h1.x, i), jp = rdl(h1.y, i);
         const int t = t_ret_old + i;

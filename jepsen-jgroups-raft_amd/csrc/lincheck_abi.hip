@@ -167,7 +167,7 @@ struct lc_plan {
   std::vector<int> dense_c;
   int dgrid_c = 0;
   int ctab_maxw = CTAB_LMAX;  // LC_CTAB_MAXW (0: counters take the grid kernel, tests)
-  int ctab_pipe = 1;          // LC_CTAB_PIPE: bit 0 double-buffered tables
+  int ctab_pipe = 3;          // LC_CTAB_PIPE: bit 0 double-buffered tables, bit 1 chunks from an LDS counter
   DevArray d_cstats;
   DevArray d_dpack, d_dwords, d_dqueue, d_dstatus, d_dfail, d_dexpl;
   // histories wider than the LDS tile teams hold: tables in HBM (wide.hip)
@@ -412,7 +412,7 @@ struct lc_plan {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
-    ctab_maxw = CTAB_LMAX, ctab_pipe = 1, wide_watchdog_ms = 20000, wide_force_abort = false;
+    ctab_maxw = CTAB_LMAX, ctab_pipe = 3, wide_watchdog_ms = 20000, wide_force_abort = false;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.2, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 12, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, rot_chain_min = 14, batch_hist = 600, mid_maxw = 0;
