@@ -409,28 +409,37 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
         if (lane == 0) c = atomicAdd(&sChunk[s & 1], 1u);
         return 64u * (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
       };
-      uint32_t f0 = dyn ? fetch() : (uint32_t)(tt & ~63);
-      for (; f0 < total;) {
-        const uint32_t f_next = dyn ? fetch() : f0 + (uint32_t)CT_TEAM;
-        const uint32_t f_this = f0;
-        f0 = f_next;
-#ifdef LC_CT_WORDPROF
-        const unsigned long long tpw = prof ? __builtin_amdgcn_s_memtime() : 0;
-#endif
+      // chunk f's segment (wave-uniform) and this lane's word of it (~0u past the segment's end);
+      // the next chunk's word is loaded while this one runs (the word list of a 14-hi-bit table
+      // is in global memory)
+      auto chunk_word = [&](uint32_t f, int& seg) -> uint32_t {
         int i = 0;
         uint32_t e = 0, acc = 0;
         for (uint64_t m = segm; m; m &= m - 1) {
           const int k = (int)__builtin_ctzll(m);
-          if (f_this >= acc) i = k, e = acc;
+          if (f >= acc) i = k, e = acc;
           acc += (rdl(nq_l, k) + 63u) & ~63u;
         }
-        const uint32_t nq = rdl(nq_l, i), r = f_this - e + (uint32_t)lane;
+        seg = i;
+        const uint32_t r = f - e + (uint32_t)lane;
+        return r < rdl(nq_l, i) ? words[rdl(o_l, i) + r] : ~0u;
+      };
+      uint32_t f0 = dyn ? fetch() : (uint32_t)(tt & ~63);
+      int seg_n = 0;
+      uint32_t w_n = f0 < total ? chunk_word(f0, seg_n) : ~0u;
+      for (; f0 < total;) {
+        const uint32_t f_next = dyn ? fetch() : f0 + (uint32_t)CT_TEAM;
+        f0 = f_next;
+#ifdef LC_CT_WORDPROF
+        const unsigned long long tpw = prof ? __builtin_amdgcn_s_memtime() : 0;
+#endif
+        const int i = seg_n;
+        const uint32_t w = w_n;
+        if (f_next < total) w_n = chunk_word(f_next, seg_n);
         const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i);
         const int j = rdl(h1.x, i), jp = rdl(h1.y, i);
         const int t = t_ret_old + i;
-        if (r >= nq) continue;
-        const uint32_t w = words[rdl(o_l, i) + r];
-        if (w & ~(live >> CTAB_LO)) continue;
+        if (w & ~(live >> CTAB_LO)) continue;  // (~0u: past the segment's end)
         CStep* st = &sRing[t % CT_RING];
         uint64_t* const Bt = tab(t);
 #ifdef LC_CT_WORDPROF
