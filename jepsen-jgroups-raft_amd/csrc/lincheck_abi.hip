@@ -879,12 +879,14 @@ struct lc_plan {
   int rot_chain_min = 14;  // LC_TEAM_ROT_CHAIN_MIN: ... and of the smaller tile sizes down to this one
   // rotation keeps slots 0..2 in the word (the encoder's slot policy; LC_SLOTS=lff: rotate them too)
   bool rot_keep_inword = !(getenv("LC_SLOTS") && strcmp(getenv("LC_SLOTS"), "lff") == 0);
-  // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7); by default 14 for
+  // LC_MID_MAXW: widest MID history when they run in big workgroups (bit 7); by default 13 for
   // a batch plan (four per CU is the cheaper throughput) and 12 for a chain plan, where a MID
   // team's longer step (w14: 7.7 us against 4.9 as a BLOCK team) becomes a chain of its own
-  // (r2cd: 4-way shares 9.92 -> 9.67 ms at the slowest rank)
+  // (r2cd: 4-way shares 9.92 -> 9.67 ms at the slowest rank). r4r LC_DEBUG on C3: the MID pool
+  // ended at 10.5 ms (its w14 histories at 8.0 us per step), the BLOCK pool at 8.1, the WAVE pool
+  // at 5.6; with w14 histories as BLOCK teams (r4s, twice each) C3 11.00-11.08 -> 10.70-10.71 ms
   int mid_maxw = 0;
-  int mid_width() const { return mid_maxw > 0 ? mid_maxw : batch_plan() ? 14 : 12; }
+  int mid_width() const { return mid_maxw > 0 ? mid_maxw : batch_plan() ? 13 : 12; }
   // LC_PLAN_K: scales the team model's VALU term. The model was fitted on unrotated teams;
   // rotated teams (auto from lb 16) spread every step over the tiles, so fewer tiles serve. A
   // batch plan (many histories sharing the chip) is throughput-bound and wants them (r2rot4/5
