@@ -51,7 +51,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = True):
+def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = True, reps: int = 1):
     """Time the CPU oracle (a C restatement of knossos.linear, test infrastructure) on the
     same workload in the same run; returns (cpu dict, oracle results, checked keys, checked
     history).
@@ -73,13 +73,20 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = True
         stride = max(1, n // 50)
         sample = list(range(n)) if full else list(range(0, n, stride))
         hs = h.select(sample)
-        t0 = time.perf_counter()
-        res = oracle.check_many(model, hs, n_threads=threads)
-        wall = time.perf_counter() - t0
+        walls = []
+        for rep in range(max(1, reps)):  # the same deterministic searches: keep the fastest pass
+            t0 = time.perf_counter()
+            r_rep = oracle.check_many(model, hs, n_threads=threads)
+            walls.append(time.perf_counter() - t0)
+            log(f"[cpu baseline] pass {rep}: {walls[-1]:.2f}s")
+            if walls[-1] == min(walls):
+                res = r_rep
+        wall = min(walls)
         per = np.array([r["wall_ns"] for r in res], np.float64) / 1e9
         desc = (f"the whole workload: all {n} keys" if full or stride == 1 else
                 f"every {stride}th key ({len(sample)} of {n}: 0, {stride}, ...; a quick sample)") + \
-            f", {threads} threads taking keys in key order from a shared counter"
+            f", {threads} threads taking keys in key order from a shared counter" + \
+            (f"; the fastest of {len(walls)} passes" if len(walls) > 1 else "")
         used = threads
         keys = {"min_s": round(float(per.min()), 5), "median_s": round(float(np.median(per)), 5),
                 "max_s": round(float(per.max()), 4), "sum_s": round(float(per.sum()), 4),
@@ -111,6 +118,7 @@ def cpu_baseline(h, model: str, budget_s: float, threads: int, full: bool = True
     if keys is not None:
         # the sample's wall is max(sum / threads, slowest key): a key's search is one thread
         out["per_key"] = keys
+        out["pass_walls_s"] = [round(w, 3) for w in walls]
     return out, res, sample, hs
 
 
@@ -384,6 +392,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", action="store_true",
                     help="cpu_baseline on every 20th key only (quick; the default is every key)")
+    ap.add_argument("--cpu-reps", type=int, default=2,
+                    help="whole-workload CPU passes; the fastest is quoted (r4u: one pass of two "
+                         "ran 31 %% slow, its slowest key 53 s against 39 s in every other pass)")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="lc_check calls from host arrays timed after the run (0: skip)")
     ap.add_argument("--e2e-shards", type=int, default=8,
@@ -611,7 +622,8 @@ def main():
     parity = None
     if not args.no_cpu and world == 1 and not args.emulate:
         ci = cpu_info()
-        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, ci["threads"], not args.cpu_sample)
+        cpu, ores, sample, hs = cpu_baseline(h, model, args.cpu_budget, ci["threads"], not args.cpu_sample,
+                                             args.cpu_reps if not args.cpu_sample else 1)
         cpu.update({k: ci[k] for k in ("cpu_model", "nproc", "affinity")})
         cpu["cores_from"] = ci["share"]
         if h.n_hist > 1:
