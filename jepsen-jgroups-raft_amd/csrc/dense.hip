@@ -1810,6 +1810,15 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
   __shared__ uint32_t sCum[BINOM_N * BINOM_N];  // sCum[n][k] = sum of C(n, q) for q < k
 
   const int tid = threadIdx.x, lane = tid & 63;
+  // LC_DEBUG: the workgroup's shader-clock and 100-MHz-clock spans (their ratio: the core clock
+  // the chains ran at), summed over workgroups
+  const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+  auto note_clock = [&]() {
+    if (p.lhist && tid == 0) {
+      atomicAdd(&p.lhist[64 * LH_N + 30], __builtin_amdgcn_s_memtime() - clk0);
+      atomicAdd(&p.lhist[64 * LH_N + 31], __builtin_amdgcn_s_memrealtime() - rt0);
+    }
+  };
   init_tables(sBinom, sWOff, DENSE_WORD_BITS, 1024);
   for (int i = tid; i < BINOM_N * BINOM_N; i += 1024) {
     uint32_t c = 0;
@@ -1853,6 +1862,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
       history_loop<1024, DENSE_LMAX>(p, sTab, &sZero, sOp, &sQ, &sRed, p.words, sWOff, sBinom, tid, st_fout,
                                      st_steps);
     if (p.n_w > 0) big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);  // then the WAVE queue
+    note_clock();
     flush_stats(p, st_fout, st_steps, tid == 0);
     return;
   }
@@ -1903,6 +1913,7 @@ __global__ void __launch_bounds__(1024) dense_big_kernel(DenseParams p) {
                                                st_fout, st_steps);
     if (p.n2 > 0 && (p.pipe & 128)) big_mid_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
     if (p.n_w > 0) big_wave_mode(p, sTab, &sZero, sBinom, tid, st_fout, st_steps);
+    note_clock();
     flush_stats(p, st_fout, st_steps, tid == 0);
     return;
   }

@@ -1327,6 +1327,9 @@ struct lc_plan {
                     "decode+start %.0f barrier %.0f (%.0f super-layers)\n", kind == 0 ? "WAVE" : kind == 1 ? "BLOCK" : "MID",
                     wv == 0 ? "wave 0" : "decoder wave", q[0] / n, q[1] / n, q[2] / n, q[3] / n, n);
           }
+      if (LH[64 * LH_N + 31])  // the big kernel's workgroups: shader clock over the 100-MHz clock
+        fprintf(stderr, "[lincheck]   big kernel: mean core clock %.0f MHz over its workgroups' lifetimes\n",
+                100.0 * (double)LH[64 * LH_N + 30] / (double)LH[64 * LH_N + 31]);
       if (hipMemcpy(LH.data(), d_dlhist.p, LH.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
         for (int k = 0; k < 64; ++k) {
           const unsigned long long* e = &LH[k * LH_N];
