@@ -170,6 +170,7 @@ struct lc_plan {
   int ctab_pipe = 3;          // LC_CTAB_PIPE: bit 0 double-buffered tables, bit 1 chunks from an LDS counter
   DevArray d_cstats;
   DevArray d_dpack, d_dwords, d_dqueue, d_dstatus, d_dfail, d_dexpl;
+  DevArray d_dres;  // run_dense's results in one block: explored | status | fail | stats | abort | stamps
   // histories wider than the LDS tile teams hold: tables in HBM (wide.hip)
   std::vector<int> dense_wd;
   std::vector<char> wide_ok;
@@ -1004,12 +1005,18 @@ struct lc_plan {
     const int nm = (int)dense_m.size();
     if (nb + nw + nx + nm == 0) return 0;
     const int n = enc.n_hist;
-    // one stats block per kernel: big, wave, MID
-    HIP_TRY(d_stats.ensure(3 * SS_N * 8));
-    ZeroSpans z0;  // (one launch; the abort word joins it below)
+    // the results in ONE device block, copied back in one transfer: explored (8 B per history) |
+    // status (4) | fail step (4) | one stats block per kernel (big, wave, MID) | the abort word |
+    // per-history start / end stamps (32; the chain-bound figure, stats 39..41)
+    const size_t n1 = (size_t)std::max(n, 1);
+    const size_t o_st = n1 * 8, o_fs = o_st + n1 * 4, o_ss = (o_fs + n1 * 4 + 7) & ~(size_t)7,
+                 o_ab = o_ss + 3 * SS_N * 8, o_sp = o_ab + 16, r_bytes = o_sp + n1 * 32;
+    HIP_TRY(d_dres.ensure(r_bytes));
+    char* const rb = (char*)d_dres.p;
+    ZeroSpans z0;  // (one launch)
     z0.add(d_dqueue.p, 16);
-    z0.add(d_stats.p, 3 * SS_N * 8);
-    z0.add(d_dexpl.p, (size_t)std::max(n, 1) * 8);
+    z0.add(rb, n1 * 8);                          // explored
+    z0.add(rb + o_ss, 3 * SS_N * 8 + 16 + n1 * 32);  // stats, abort word, stamps
     DenseParams p{};
     p.sbeg = dp_sbeg;
     p.nsteps = dp_nst;
@@ -1017,15 +1024,12 @@ struct lc_plan {
     p.words = d_dwords.as<uint32_t>();
     p.stream = dp_stream;
     p.stream_words = dstream_words;
-    p.status = d_dstatus.as<int32_t>();
-    p.fail_step = d_dfail.as<int32_t>();
-    p.explored = d_dexpl.as<unsigned long long>();
-    p.stats = d_stats.as<unsigned long long>();
+    p.status = (int32_t*)(rb + o_st);
+    p.fail_step = (int32_t*)(rb + o_fs);
+    p.explored = (unsigned long long*)rb;
+    p.stats = (unsigned long long*)(rb + o_ss);
     p.pipe = dense_pipe;
-    // per-history start / end stamps (always: the chain-bound figure, stats 39..41)
-    HIP_TRY(d_dstamps.ensure((size_t)std::max(n, 1) * 32));
-    z0.add(d_dstamps.p, (size_t)std::max(n, 1) * 32);
-    p.stamps = d_dstamps.as<unsigned long long>();
+    p.stamps = (unsigned long long*)(rb + o_sp);
     if (debug()) {
       HIP_TRY(d_dlhist.ensure((64 * LH_N + 32) * 8));
       HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, (64 * LH_N + 32) * 8, stream));
@@ -1107,13 +1111,11 @@ struct lc_plan {
       HIP_TRY(d_tanyoff.ensure(max_teams * 4));
       HIP_TRY(d_tflags.ensure(max_wgs * 8));
       HIP_TRY(d_ctl.ensure(max_teams * dense_ctl_bytes()));
-      HIP_TRY(d_abort.ensure(16));
       HIP_TRY(d_wgteam.ensure(max_wgs * 4));
       HIP_TRY(d_tbase.ensure(max_teams * 4));
       HIP_TRY(d_tbits.ensure(max_teams));
       HIP_TRY(d_tlbits.ensure(max_teams));
       HIP_TRY(d_thist.ensure(max_teams * 4));
-      z0.add(d_abort.p, 16);
     }
     HIP_TRY(zero_spans(z0, stream));
     // LC_PIPE bit 6 (default): WAVE histories run on the big kernel's waves after its BLOCK queue
@@ -1126,7 +1128,7 @@ struct lc_plan {
       q.n = nw;
       q.order = dp_ord + nb;
       q.queue = d_dqueue.as<int32_t>() + 1;
-      q.stats = d_stats.as<unsigned long long>() + SS_N;
+      q.stats = p.stats + SS_N;
       HIP_TRY(hipEventRecord(ev_w0, stream2));
       HIP_TRY(launch_dense(q, DENSE_WAVE, std::min(dgrid_w, (nw + 3) / 4), stream2));
       HIP_TRY(hipEventRecord(ev_w1, stream2));
@@ -1141,7 +1143,7 @@ struct lc_plan {
       q.n = nm;
       q.order = dp_ord + nb + nw + nx;
       q.queue = d_dqueue.as<int32_t>() + 2;
-      q.stats = d_stats.as<unsigned long long>() + 2 * SS_N;
+      q.stats = p.stats + 2 * SS_N;
       HIP_TRY(hipEventRecord(ev_m0, stream3));
       // wave + MID workgroups stay within one per CU: either fits beside a big-kernel
       // workgroup, two of them do not, and every tile-team workgroup must be resident
@@ -1211,7 +1213,7 @@ struct lc_plan {
         }
         q.flags = d_tflags.as<unsigned long long>();
         q.ctl = d_ctl.p;
-        q.abort = d_abort.as<int32_t>();
+        q.abort = (int32_t*)(rb + o_ab);
         if (debug() && l == 0) {
           HIP_TRY(d_tstamps.ensure((size_t)twgs * 64));
           HIP_TRY(hipMemsetAsync(d_tstamps.p, 0, (size_t)twgs * 64, stream));
@@ -1235,33 +1237,25 @@ struct lc_plan {
     if (nw && !wave_in_big) HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
     if (nm && !mid_in_big) HIP_TRY(hipStreamWaitEvent(stream, ev_join3, 0));
     HIP_TRY(hipEventRecord(ev1, stream));
+    // the result block into one pinned buffer: one transfer behind the kernels, one wait
+    if (hstage_bytes < r_bytes) {
+      if (hstage) HIP_TRY(hipHostFree(hstage));
+      hstage = nullptr;
+      HIP_TRY(hipHostMalloc(&hstage, r_bytes, hipHostMallocDefault));
+      hstage_bytes = r_bytes;
+    }
+    char* const hb = reinterpret_cast<char*>(hstage);
+    HIP_TRY(hipMemcpyAsync(hb, rb, r_bytes, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     float t = 0;
     HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
     *ms += t;
-    // the results (explored, status, fail step, stats, abort word) into one pinned buffer,
-    // copied back-to-back and waited on once
-    const size_t need = (size_t)n * 48 + 3 * SS_N * 8 + 16;
-    if (hstage_bytes < need) {
-      if (hstage) HIP_TRY(hipHostFree(hstage));
-      hstage = nullptr;
-      HIP_TRY(hipHostMalloc(&hstage, need, hipHostMallocDefault));
-      hstage_bytes = need;
-    }
-    unsigned long long* const ex = hstage;
-    int32_t* const st = reinterpret_cast<int32_t*>(hstage + n);
-    int32_t* const fs = st + n;
-    unsigned long long* const ss3 = reinterpret_cast<unsigned long long*>(fs + n);  // (16 n bytes in)
-    int32_t* const abw = reinterpret_cast<int32_t*>(ss3 + 3 * SS_N);
-    unsigned long long* const stamp = reinterpret_cast<unsigned long long*>(ss3 + 3 * SS_N + 2);
-    HIP_TRY(hipMemcpyAsync(stamp, d_dstamps.p, (size_t)n * 32, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(ex, d_dexpl.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(st, d_dstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(fs, d_dfail.p, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(ss3, d_stats.p, 3 * SS_N * 8, hipMemcpyDeviceToHost, stream));
-    *abw = 0;
-    if (max_wgs) HIP_TRY(hipMemcpyAsync(abw, d_abort.p, 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    const unsigned long long* const ex = reinterpret_cast<const unsigned long long*>(hb);
+    const int32_t* const st = reinterpret_cast<const int32_t*>(hb + o_st);
+    const int32_t* const fs = reinterpret_cast<const int32_t*>(hb + o_fs);
+    const unsigned long long* const ss3 = reinterpret_cast<const unsigned long long*>(hb + o_ss);
+    const int32_t* const abw = reinterpret_cast<const int32_t*>(hb + o_ab);
+    const unsigned long long* const stamp = reinterpret_cast<const unsigned long long*>(hb + o_sp);
     if (*abw) {
       last_error = "dense tile-team watchdog fired (a team workgroup was not resident)";
       return LC_E_INTERNAL;
@@ -1315,7 +1309,7 @@ struct lc_plan {
       fprintf(stderr, "[lincheck] dense: %d block + %d wave + %d tile-team histories (%zu launch(es), %zu team "
               "workgroups): %.3f ms, steps=%llu Fout=%llu\n", nb, nw, nx, launches.size(), max_wgs, t,
               ss[SS_STEPS], ss[SS_FOUT]);
-      dense_report();
+      dense_report(stamp);
       std::vector<unsigned long long> LH(64 * LH_N + 32);
       if (hipMemcpy(LH.data(), d_dlhist.p, LH.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
         for (int kind = 0; kind < 3; ++kind)
@@ -1362,10 +1356,7 @@ struct lc_plan {
   }
 
   // LC_DEBUG: per-team spans and the slowest histories (s_memrealtime, 100 MHz)
-  void dense_report() {
-    const int n = enc.n_hist;
-    std::vector<unsigned long long> T((size_t)n * 4);
-    if (hipMemcpy(T.data(), d_dstamps.p, T.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  void dense_report(const unsigned long long* T) {  // T: the host copy of the stamps [n][4]
     const std::vector<int>* lists[4] = {&dense_b, &dense_w, &dense_x, &dense_m};
     const char* names[4] = {"block", "wave", "wide", "mid"};
     unsigned long long t0 = ~0ull;
