@@ -487,6 +487,29 @@ constexpr int PIPE_REG_FIX = 2048;  // REG histories: the closure as a whole-tab
 constexpr int REG_FIX_MAXL = 7;
 constexpr int REG_LMAX = 9;
 
+// Lane i <- lane i ^ 2^b of a 64-bit value, b a compile-time constant (REG histories: word w in
+// lane w). b <= 3 stays inside a 16-lane row and is a DPP move (quad_perm for 1 and 2,
+// row_half_mirror then quad_perm 3 for 4, row_ror 8 for 8): a VALU op instead of ds_bpermute's LDS
+// round trip on every fixpoint iteration; wider distances keep the shuffle.
+template <int B>
+__device__ __forceinline__ uint64_t lane_xor(uint64_t v) {
+  auto dpp = [](uint32_t x) -> uint32_t {
+    if constexpr (B == 0) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+    else if constexpr (B == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);
+    else if constexpr (B == 2)
+      return (uint32_t)__builtin_amdgcn_update_dpp(
+          0, __builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false), 0x1B, 0xF, 0xF, false);
+    else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);
+  };
+  if constexpr (B <= 3) return ((uint64_t)dpp((uint32_t)(v >> 32)) << 32) | dpp((uint32_t)v);
+  else return (uint64_t)__shfl_xor((unsigned long long)v, 1 << B, 64);
+}
+template <int B>
+__device__ __forceinline__ uint64_t lane_xor_dyn(uint64_t v, int b) {  // b == B..REG_LMAX-4, unrolled
+  if constexpr (B >= 6) return v;
+  else return b == B ? lane_xor<B>(v) : lane_xor_dyn<B + 1>(v, b);
+}
+
 // close_in_word with the in-word ops and the returning op's passed by value (no indexed array)
 __device__ __forceinline__ uint64_t close_in_word_r(uint64_t X, uint32_t w, uint32_t live, int j, OpSel o0,
                                                    OpSel o1, OpSel o2, uint32_t foldm, uint64_t R) {
@@ -575,7 +598,7 @@ __device__ __forceinline__ void run_regs(const DenseParams& p, int h, OpSel* opt
 #pragma unroll
         for (int b = 0; b < REG_LMAX - 3; ++b) {
           if (b >= H) break;
-          const uint64_t v = (uint64_t)__shfl_xor((unsigned long long)B, 1 << b, 64) & notj64;
+          const uint64_t v = lane_xor_dyn<0>(B, b) & notj64;
           if ((pm >> b) & 1u) Rn |= transfer(oh[b], (foldm >> (b + 3)) & 1u, v);
         }
         if (!holds_j) {
@@ -598,7 +621,7 @@ __device__ __forceinline__ void run_regs(const DenseParams& p, int h, OpSel* opt
 #pragma unroll
       for (int b = 0; b < REG_LMAX - 3; ++b) {
         if (b >= H) break;
-        const uint64_t v = (uint64_t)__shfl_xor((unsigned long long)Bw, 1 << b, 64);
+        const uint64_t v = lane_xor_dyn<0>(Bw, b);
         if ((pm >> b) & 1u) R |= transfer(oh[b], (foldm >> (b + 3)) & 1u, v);
       }
       R = close_in_word_r(Bw, w, live, j, o0, o1, o2, foldm, R);
