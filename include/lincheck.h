@@ -217,7 +217,7 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  *    hipSetDevice, 22 streams/events/occupancy queries, 23 uploads, 24 dense step streams
  * 25..27 dense big kernel: frontier configs in, frontier configs out, configs explored
  * 28..30 the same for the dense wave (+ MID) kernel
- * 31 histories decided on closure tables in HBM (wide.hip: live width 25..31; counted in 12 too)
+ * 31 histories decided on closure tables in HBM (wide.hip: live width 25..35; counted in 12 too)
  * 32 their kernel's ms (part of 0 and 13)
  * 33 their algorithmic HBM bytes: per step and live word, its X, its pulls and its store (8 B each)
  * 34 counter histories decided on closure tables (ctab.hip; counted in 12 too)  35 their kernel's ms

@@ -1051,13 +1051,13 @@ def test_gpu_bench_two_ranks_one_gpu(workload, tmp_path):
         assert out["verdict"]["bounds_ok"] is True
 
 
-# ---- closure tables in HBM (wide.hip): live width 25..31 -------------------
+# ---- closure tables in HBM (wide.hip): live width 25..35 -------------------
 
 @pytest.mark.parametrize("pipe,grid", [("1", "0"), ("0", "0"), ("1", "8")])
 @pytest.mark.parametrize("minw", ["1", "12"])
 def test_gpu_wide_tables_vs_oracle(minw, pipe, grid, monkeypatch):
     """The HBM-table kernel, with LC_WIDE_MINW routing every history from that width on to it
-    (in production it takes widths 25..31 only): random histories valid and invalid, 16-client
+    (in production it takes widths 25..35 only): random histories valid and invalid, 16-client
     histories with crashed ops, the low-slot orderings and tiny/empty ones, one launch for all
     of them, bit-exact with the oracle (verdict, failing op, its invocation, :previous-ok,
     explored). LC_WIDE_PIPE=1 (the default) overlaps consecutive steps on the grid, 0 runs one
