@@ -1,0 +1,47 @@
+"""CPU tests of bench.py's host-side pieces (no GPU): the cpu_baseline leg (the whole workload,
+the fastest of several passes, the per-key figures beside it) and the whole-history fixtures
+the single-history lines quote."""
+import importlib.util
+import os
+
+import pytest
+
+from lincheck import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_cpu_baseline_whole_workload_fastest_pass(bench):
+    h = synth.gen_config("c1")
+    cpu, res, sample, hs = bench.cpu_baseline(h, "cas-register", 1.0, 2, full=True, reps=2)
+    assert sample == list(range(h.n_hist)) and len(res) == h.n_hist
+    assert len(cpu["pass_walls_s"]) == 2
+    assert cpu["wall_s"] == pytest.approx(min(cpu["pass_walls_s"]), abs=1e-3)
+    w = cpu["wall_s"]  # (rounded to 1 ms)
+    assert hs.n_ops() / (w + 6e-4) <= cpu["value"] <= hs.n_ops() / max(w - 6e-4, 1e-9)
+    assert "fastest of 2 passes" in cpu["sample"] and cpu["cores"] == 2
+    pk = cpu["per_key"]
+    assert pk["max_s"] <= pk["sum_s"] and pk["wall_bound_s"] == pytest.approx(max(pk["sum_s"] / 2, pk["max_s"]),
+                                                                                abs=1e-3)
+
+
+def test_cpu_baseline_quick_sample_is_one_pass(bench):
+    h = synth.gen_config("c3", scale=0.1)
+    cpu, res, sample, hs = bench.cpu_baseline(h, "cas-register", 1.0, 2, full=False, reps=1)
+    assert len(cpu["pass_walls_s"]) == 1 and "a quick sample" in cpu["sample"]
+    assert sample == list(range(0, h.n_hist, max(1, h.n_hist // 50)))
+
+
+@pytest.mark.parametrize("workload", ["c4", "c2c", "c2c4", "c5x"])
+def test_golden_fixture_for_single_history_lines(bench, workload):
+    fx = bench.golden_fixture(workload)
+    assert fx is not None and fx["explored"] > 0 and fx["provenance"]["wall_s"] > 0
+    assert bench.golden_fixture("c3") is None
