@@ -384,7 +384,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--workload", default="c3", choices=sorted(MODEL_OF))
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests)")
     ap.add_argument("--cpu-budget", type=float, default=6.0,
