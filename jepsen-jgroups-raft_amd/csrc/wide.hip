@@ -101,6 +101,63 @@ __device__ __forceinline__ uint64_t wide_pulls(const uint64_t* B, uint32_t w, ui
   return R;
 }
 
+// ---- the pipelined kernel's table layout: word w (hi bits of one step, all < 2^Hm) lives at
+// off[|w|] + colex(w), off[q] = sum_{p < q} C(Hm, p) and colex(w) = sum_i C(pos_i, i + 1) over
+// w's set bits in ascending order (i = 0, 1, ...): its index among the words of its popcount in
+// ascending order. A layer's words are one contiguous span, and a run of consecutive low words
+// under one high part (how the kernel hands words to threads) is a run of consecutive addresses.
+__device__ __forceinline__ uint32_t colex_rank(uint32_t w, const uint32_t* bin) {
+  uint32_t r = 0;
+  for (int i = 1; w; ++i, w &= w - 1) r += bin[__builtin_ctz(w) * WB + i];
+  return r;
+}
+
+// wide_pulls over the ranked layout: the pull of bit b_m (the m-th set bit of w) reads
+// off[|w| - 1] + sum_{i < m} C(pos_i, i + 1) + sum_{i > m} C(pos_i, i)
+__device__ __forceinline__ uint64_t wide_pulls_ranked(const uint64_t* B, uint32_t w, uint32_t jh, const OpSel* ops,
+                                                     uint64_t foldm, const uint32_t* bin, uint32_t off_dn) {
+  uint32_t m = (w & jh) ? jh : w;
+  uint32_t T0 = 0;  // sum_i C(pos_i, i)
+  {
+    uint32_t x = w;
+    for (int i = 0; x; ++i, x &= x - 1) T0 += bin[__builtin_ctz(x) * WB + i];
+  }
+  uint32_t x = w, P1 = 0, P0 = 0;  // (x: w's bits not yet passed; P1, P0 over the passed ones)
+  int i = 0;
+  uint64_t R = 0;
+  while (m) {
+    int bb[8];
+    uint32_t ix[8];
+    uint64_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      bb[u] = -1;
+      ix[u] = 0;
+      if (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1;
+        for (uint32_t below = x & ((1u << b) - 1u); below; below &= below - 1, ++i) {
+          const int pos = __builtin_ctz(below);
+          P1 += bin[pos * WB + i + 1];
+          P0 += bin[pos * WB + i];
+        }
+        x &= ~((2u << b) - 1u);
+        P0 += bin[b * WB + i];
+        ix[u] = off_dn + P1 + (T0 - P0);
+        P1 += bin[b * WB + i + 1];
+        ++i;
+        bb[u] = b;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = bb[u] >= 0 ? HbmTab::ld(&B[ix[u]]) : 0ull;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (bb[u] >= 0) R |= transfer(ops[bb[u] + 3], (foldm >> (bb[u] + 3)) & 1u, v[u]);
+  }
+  return R;
+}
+
 __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
   __shared__ uint32_t sBin[WB * WB];
   __shared__ uint32_t sPre[(WH + 1) * WPRE];
@@ -285,9 +342,16 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
 // A super-layer's words are the running steps' layers, one flat index over the grid; a layer's
 // word g is (high part, low part) by popcount of the high part p (C(hb, p) highs of popcount p,
 // each with C(k, q - p) lows; both parts from the sorted word list), so no per-layer tables.
+// Its tables use the ranked layout (colex_rank): word w at off[|w|] + colex(w).
 // Failure: a workgroup that reads a nonzero X in step t sets bit t of `anyv`; when step t retires
 // (after its last layer's barrier) every workgroup reads the bit: 0 means step t - 1 returned an
 // empty frontier.
+#ifndef LC_WIDE_KLO
+#define LC_WIDE_KLO 19
+#endif
+#ifndef LC_WIDE_XCD
+#define LC_WIDE_XCD 1
+#endif
 constexpr int WRING = 16;
 struct WStep {
   OpSel ops[WIDE_OPS];
@@ -300,6 +364,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
   __shared__ uint32_t sLay[WIDE_LOW_BITS + 2];
   __shared__ WStep sRing[WRING];
   __shared__ uint32_t sSeg[WRING + 1];  // running segments' first flat index (+ the total)
+  __shared__ uint32_t sOff[WH + 2];     // the ranked layout's layer offsets (colex_rank)
   __shared__ unsigned long long sRed;
   __shared__ int sAbort;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -319,7 +384,18 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
     for (int r = 0; r < tid; ++r) o += sBin[DENSE_WORD_BITS * WB + r];
     sLay[tid] = o;
   }
-  const int64_t gtid = (int64_t)blockIdx.x * WWG + tid, gstride = (int64_t)gridDim.x * WWG;
+  if (tid <= WH + 1) {
+    const int Hm = 63 - __clzll((long long)p.tab_words);  // (tab_words = 2^Hm)
+    uint32_t o = 0;
+    for (int r = 0; r < tid && r <= Hm; ++r) o += sBin[Hm * WB + r];
+    sOff[tid] = o;
+  }
+  // XCD-aware chunks: workgroups are dealt to the 8 XCDs round robin, so logical block
+  // (b mod 8) * (grid / 8) + b / 8 gives each XCD one contiguous run of a super-layer's words per
+  // pass (a high part's words and their low-bit pulls stay in one L2)
+  const int nb = (int)gridDim.x, bx = (int)blockIdx.x;
+  const int lb = (nb & 7) == 0 && LC_WIDE_XCD ? (bx & 7) * (nb >> 3) + (bx >> 3) : bx;
+  const int64_t gtid = (int64_t)lb * WWG + tid, gstride = (int64_t)gridDim.x * WWG;
   unsigned long long st_fout = 0, st_steps = 0, st_wv = 0, st_wnz = 0;
   for (int i = 0; i < p.n && !sAbort; ++i) {
     const int ns = p.nsteps[i];
@@ -395,7 +471,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
         const int t = t_ret + si;
         const WStep& r = sRing[t % WRING];
         const int H = r.H, q = s - r.start;
-        const int k = H < WIDE_LOW_BITS ? H : WIDE_LOW_BITS, hb = H - k;
+        const int k = max(H < LC_WIDE_KLO ? H : LC_WIDE_KLO, H - WIDE_LOW_BITS), hb = H - k;
         uint32_t gi = (uint32_t)g - sSeg[si];
         int pp = q - k > 0 ? q - k : 0;  // the high part's popcount: blocks of C(hb, p) C(k, q - p)
         for (;; ++pp) {
@@ -411,19 +487,20 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
         const uint64_t fresh = r.fresh, foldm = r.foldm;
         const int j = (int)r.j, jp = r.jp;
         uint64_t X = 0;
+        const uint32_t iw = sOff[q] + colex_rank(w, sBin);  // (|w| = q)
         if (!(w & (fresh >> 3))) {
           const uint64_t* Bp = tab(t - 1);
-          if (jp >= 3) X = HbmTab::ld(&Bp[w | (1u << (jp - 3))]);
-          else if (jp >= 0) X = (HbmTab::ld(&Bp[w]) & ~keep64(jp)) >> (1 << jp);
-          else X = HbmTab::ld(&Bp[w]);
+          if (jp >= 3) X = HbmTab::ld(&Bp[sOff[q + 1] + colex_rank(w | (1u << (jp - 3)), sBin)]);
+          else if (jp >= 0) X = (HbmTab::ld(&Bp[iw]) & ~keep64(jp)) >> (1 << jp);
+          else X = HbmTab::ld(&Bp[iw]);
 #pragma unroll
           for (int kk = 0; kk < 3; ++kk)
             if (fresh & (1u << kk)) X &= keep64(kk);
         }
         uint64_t* const B = tab(t);
-        uint64_t R = wide_pulls(B, w, j >= 3 ? 1u << (j - 3) : 0u, r.ops, foldm);
+        uint64_t R = wide_pulls_ranked(B, w, j >= 3 ? 1u << (j - 3) : 0u, r.ops, foldm, sBin, q > 0 ? sOff[q - 1] : 0u);
         R = close_in_word(X, w, (uint32_t)live, j, r.ops, (uint32_t)foldm, R);
-        HbmTab::st(&B[w], X | R);
+        HbmTab::st(&B[iw], X | R);
         expl += (uint64_t)__popcll(R);
         if (t > 0) st_fout += (uint64_t)__popcll(X);
         if (X) anyseg |= 1u << si;
@@ -469,9 +546,9 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
       uint64_t nz = 0;
       for (int64_t w = gtid; w < nwt; w += gstride) {
         if ((uint64_t)w & ~(lv >> 3)) continue;
-        uint64_t X;
-        if (pj >= 3) X = HbmTab::ld(&Bl[(uint32_t)w | (1u << (pj - 3))]);
-        else X = (HbmTab::ld(&Bl[w]) & ~keep64(pj)) >> (1 << pj);
+        const uint32_t wr = pj >= 3 ? (uint32_t)w | (1u << (pj - 3)) : (uint32_t)w;
+        uint64_t X = HbmTab::ld(&Bl[sOff[__popc(wr)] + colex_rank(wr, sBin)]);
+        if (pj < 3) X = (X & ~keep64(pj)) >> (1 << pj);
         st_fout += (uint64_t)__popcll(X);
         nz |= X;
       }
