@@ -106,54 +106,61 @@ __device__ __forceinline__ uint64_t wide_pulls(const uint64_t* B, uint32_t w, ui
 // w's set bits in ascending order (i = 0, 1, ...): its index among the words of its popcount in
 // ascending order. A layer's words are one contiguous span, and a run of consecutive low words
 // under one high part (how the kernel hands words to threads) is a run of consecutive addresses.
-__device__ __forceinline__ uint32_t colex_rank(uint32_t w, const uint32_t* bin) {
-  uint32_t r = 0;
-  for (int i = 1; w; ++i, w &= w - 1) r += bin[__builtin_ctz(w) * WB + i];
+// (8 set bits per round: the binomial reads of a round are independent, one LDS wait per round)
+__device__ __forceinline__ uint32_t colex_rank(uint32_t w, const uint32_t* bin, uint32_t* T0 = nullptr) {
+  uint32_t r = 0, t0 = 0;
+  for (int i = 0; w; i += 8) {
+    int bb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      bb[u] = w ? __builtin_ctz(w) : -1;
+      w &= w - 1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (bb[u] >= 0) {
+        r += bin[bb[u] * WB + i + u + 1];
+        if (T0) t0 += bin[bb[u] * WB + i + u];
+      }
+  }
+  if (T0) *T0 = t0;
   return r;
 }
 
 // wide_pulls over the ranked layout: the pull of bit b_m (the m-th set bit of w) reads
-// off[|w| - 1] + sum_{i < m} C(pos_i, i + 1) + sum_{i > m} C(pos_i, i)
+// off[|w| - 1] + sum_{i < m} C(pos_i, i + 1) + sum_{i > m} C(pos_i, i); T0 = sum_i C(pos_i, i).
+// Rounds of 8 of w's set bits (up to the last pulled one): their binomials, then their pulls.
 __device__ __forceinline__ uint64_t wide_pulls_ranked(const uint64_t* B, uint32_t w, uint32_t jh, const OpSel* ops,
-                                                     uint64_t foldm, const uint32_t* bin, uint32_t off_dn) {
-  uint32_t m = (w & jh) ? jh : w;
-  uint32_t T0 = 0;  // sum_i C(pos_i, i)
-  {
-    uint32_t x = w;
-    for (int i = 0; x; ++i, x &= x - 1) T0 += bin[__builtin_ctz(x) * WB + i];
-  }
-  uint32_t x = w, P1 = 0, P0 = 0;  // (x: w's bits not yet passed; P1, P0 over the passed ones)
-  int i = 0;
+                                                     uint64_t foldm, const uint32_t* bin, uint32_t off_dn,
+                                                     uint32_t T0) {
+  const uint32_t m = (w & jh) ? jh : w;
+  uint32_t x = (w & jh) ? w & ((jh << 1) - 1u) : w;
+  uint32_t P1 = 0, P0 = 0;
   uint64_t R = 0;
-  while (m) {
+  for (int i = 0; x; i += 8) {
     int bb[8];
     uint32_t ix[8];
     uint64_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      bb[u] = -1;
-      ix[u] = 0;
-      if (m) {
-        const int b = __builtin_ctz(m);
-        m &= m - 1;
-        for (uint32_t below = x & ((1u << b) - 1u); below; below &= below - 1, ++i) {
-          const int pos = __builtin_ctz(below);
-          P1 += bin[pos * WB + i + 1];
-          P0 += bin[pos * WB + i];
-        }
-        x &= ~((2u << b) - 1u);
-        P0 += bin[b * WB + i];
-        ix[u] = off_dn + P1 + (T0 - P0);
-        P1 += bin[b * WB + i + 1];
-        ++i;
-        bb[u] = b;
+      bb[u] = x ? __builtin_ctz(x) : -1;
+      x &= x - 1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ix[u] = 0xffffffffu;
+      if (bb[u] >= 0) {
+        const uint32_t c0 = bin[bb[u] * WB + i + u], c1 = bin[bb[u] * WB + i + u + 1];
+        P0 += c0;
+        if ((m >> bb[u]) & 1u) ix[u] = off_dn + P1 + (T0 - P0);
+        P1 += c1;
       }
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = bb[u] >= 0 ? HbmTab::ld(&B[ix[u]]) : 0ull;
+    for (int u = 0; u < 8; ++u) v[u] = ix[u] != 0xffffffffu ? HbmTab::ld(&B[ix[u]]) : 0ull;
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (bb[u] >= 0) R |= transfer(ops[bb[u] + 3], (foldm >> (bb[u] + 3)) & 1u, v[u]);
+      if (ix[u] != 0xffffffffu) R |= transfer(ops[bb[u] + 3], (foldm >> (bb[u] + 3)) & 1u, v[u]);
   }
   return R;
 }
@@ -487,7 +494,8 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
         const uint64_t fresh = r.fresh, foldm = r.foldm;
         const int j = (int)r.j, jp = r.jp;
         uint64_t X = 0;
-        const uint32_t iw = sOff[q] + colex_rank(w, sBin);  // (|w| = q)
+        uint32_t T0;
+        const uint32_t iw = sOff[q] + colex_rank(w, sBin, &T0);  // (|w| = q)
         if (!(w & (fresh >> 3))) {
           const uint64_t* Bp = tab(t - 1);
           if (jp >= 3) X = HbmTab::ld(&Bp[sOff[q + 1] + colex_rank(w | (1u << (jp - 3)), sBin)]);
@@ -498,7 +506,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
             if (fresh & (1u << kk)) X &= keep64(kk);
         }
         uint64_t* const B = tab(t);
-        uint64_t R = wide_pulls_ranked(B, w, j >= 3 ? 1u << (j - 3) : 0u, r.ops, foldm, sBin, q > 0 ? sOff[q - 1] : 0u);
+        uint64_t R = wide_pulls_ranked(B, w, j >= 3 ? 1u << (j - 3) : 0u, r.ops, foldm, sBin, q > 0 ? sOff[q - 1] : 0u, T0);
         R = close_in_word(X, w, (uint32_t)live, j, r.ops, (uint32_t)foldm, R);
         HbmTab::st(&B[iw], X | R);
         expl += (uint64_t)__popcll(R);
