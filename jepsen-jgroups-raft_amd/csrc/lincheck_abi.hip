@@ -177,7 +177,7 @@ struct lc_plan {
   std::vector<std::vector<uint32_t>> wide_streams;  // per history (built by dense_sink)
   DevArray d_wtab, d_wstream, d_wmeta, d_wres, d_wbar;
   int wide_maxw = WIDE_LMAX, wide_minw = 0;  // LC_WIDE_MAXW (0: off) / LC_WIDE_MINW (tests)
-  int wide_grid = 0;  // LC_WIDE_GRID: at most this many workgroups for the HBM tables (0: one per CU)
+  int wide_grid = 0;  // LC_WIDE_GRID: at most this many workgroups for the HBM tables (0: all resident)
   int wide_watchdog_ms = 20000;  // LC_WIDE_WATCHDOG_MS: a grid barrier's longest wait
   bool wide_force_abort = false;  // LC_WIDE_FORCE_ABORT=1 (tests): the abort word set before launch
   bool wide_pipe = true;  // LC_WIDE_PIPE=0: one step at a time (a grid barrier per popcount layer)
@@ -1861,7 +1861,7 @@ struct lc_plan {
     p.bar = d_wbar.as<unsigned>();
     p.abort = (int32_t*)((char*)d_wbar.p + wide_bar_bytes());
     p.watchdog = (uint64_t)wide_watchdog_ms * 100000ull;
-    const int grid = wide_grid > 0 ? std::min(wide_grid, wide_grid_size()) : wide_grid_size();
+    const int grid = wide_grid > 0 ? std::min(wide_grid, wide_grid_size(p.pipe)) : wide_grid_size(p.pipe);
     if (grid < 1) {
       last_error = "wide kernel: no resident workgroups";
       return LC_E_INTERNAL;

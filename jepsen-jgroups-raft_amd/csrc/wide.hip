@@ -27,6 +27,16 @@ namespace lc {
 namespace {
 
 constexpr int WWG = 1024;
+#ifndef LC_WIDE_MINW_EU
+#define LC_WIDE_MINW_EU 5
+#endif
+#ifndef LC_WIDE_PWG
+#define LC_WIDE_PWG 256
+#endif
+// the pipelined kernel's workgroup: 256 threads with <= 102 VGPRs, so 5 waves per SIMD (a
+// 1024-thread workgroup holds a CU at 4)
+constexpr int WPWG = LC_WIDE_PWG;
+constexpr int WP_MINW = WPWG == 1024 ? 1 : LC_WIDE_MINW_EU;
 constexpr int WB = 33;  // binomials C(n, k) for n <= 32 (u32: C(32, 16) = 601,080,390)
 constexpr int WH = WIDE_LMAX - 3;  // most hi bits
 constexpr int WPRE = 513;          // per layer: prefix over <= 512 high parts, + the total
@@ -366,7 +376,7 @@ struct WStep {
   int32_t j, jp, H, start;
 };
 
-__global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
+__global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) {
   __shared__ uint32_t sBin[WB * WB];
   __shared__ uint32_t sLay[WIDE_LOW_BITS + 2];
   __shared__ WStep sRing[WRING];
@@ -375,7 +385,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
   __shared__ unsigned long long sRed;
   __shared__ int sAbort;
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < WB * WB; i += WWG) {
+  for (int i = tid; i < WB * WB; i += WPWG) {
     const int n = i / WB, k = i % WB;
     uint64_t c = 0;
     if (k <= n) {
@@ -402,7 +412,7 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
   // pass (a high part's words and their low-bit pulls stay in one L2)
   const int nb = (int)gridDim.x, bx = (int)blockIdx.x;
   const int lb = (nb & 7) == 0 && LC_WIDE_XCD ? (bx & 7) * (nb >> 3) + (bx >> 3) : bx;
-  const int64_t gtid = (int64_t)lb * WWG + tid, gstride = (int64_t)gridDim.x * WWG;
+  const int64_t gtid = (int64_t)lb * WPWG + tid, gstride = (int64_t)gridDim.x * WPWG;
   unsigned long long st_fout = 0, st_steps = 0, st_wv = 0, st_wnz = 0;
   for (int i = 0; i < p.n && !sAbort; ++i) {
     const int ns = p.nsteps[i];
@@ -592,17 +602,20 @@ __global__ void __launch_bounds__(WWG) wide_pipe_kernel(WideParams p) {
 
 }  // namespace
 
-int wide_grid_size() {
+int wide_grid_size(bool pipe) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel, WWG, 0) != hipSuccess || per_cu < 1) return 0;
-  int per_cu2 = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, wide_pipe_kernel, WWG, 0) != hipSuccess || per_cu2 < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pipe ? (const void*)wide_pipe_kernel
+                                                                 : (const void*)wide_kernel,
+                                                   pipe ? WPWG : WWG, 0) != hipSuccess ||
+      per_cu < 1)
     return 0;
-  return prop.multiProcessorCount;  // one workgroup per CU: every workgroup resident
+  // every workgroup resident (the grid barrier needs it): one 1024-thread workgroup per CU for
+  // the one-step kernel, as many 256-thread ones as fit for the pipelined kernel
+  return prop.multiProcessorCount * (pipe ? per_cu : 1);
 }
 
 size_t wide_bar_bytes() { return sizeof(WideBar); }
@@ -611,7 +624,7 @@ hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream) {
   WideParams q = p;
   void* args[] = {&q};
   return hipLaunchCooperativeKernel(p.pipe ? (const void*)wide_pipe_kernel : (const void*)wide_kernel, dim3(grid),
-                                    dim3(WWG), args, 0, stream);
+                                    dim3(p.pipe ? WPWG : WWG), args, 0, stream);
 }
 
 }  // namespace lc

@@ -51,7 +51,7 @@ struct WideParams {
 };
 
 hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream);
-int wide_grid_size();
+int wide_grid_size(bool pipe);
 size_t wide_bar_bytes();
 
 }  // namespace lc
