@@ -380,6 +380,63 @@ def read_profile(path, workload, scale, kname):
     return tr
 
 
+def spawn_ranks(n: int) -> int:
+    """Run this same command as n ranks under torch.distributed.run (127.0.0.1, a free port) and
+    relay rank 0's JSON line; returns the launcher's exit code. The parent never touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=dict(os.environ))
+    n_json = 0
+    for line in p.stdout:  # rank 0 prints the one JSON line; anything else goes to stderr
+        if line.startswith("{"):
+            n_json += 1
+            print(line, end="", flush=True)
+        else:
+            log(line.rstrip("\n"))
+    rc = p.wait()
+    if rc == 0 and n_json != 1:
+        log(f"[bench] expected one JSON line from rank 0, got {n_json}")
+        return 1
+    return rc
+
+
+def protocol_only(args, rank, world, dist):
+    """The rank protocol without GPU work: warmup, barrier, K timed no-op steps, barrier, MAX of
+    the elapsed time over ranks, one JSON line from rank 0 (LC_BENCH_PROTOCOL_ONLY test hook)."""
+    def barrier():
+        if dist:
+            dist[1].barrier()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        torch, td = dist
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        td.all_reduce(t, op=td.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([1], dtype=torch.int64)
+        td.all_reduce(r)
+        ranks_seen = int(r.item())
+    else:
+        ranks_seen = 1
+    if rank == 0:
+        print(json.dumps({"metric": "protocol-only (test hook)", "value": 0.0, "n_gpus": world,
+                          "ranks_seen": ranks_seen, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / max(1, args.steps) * 1e3}), flush=True)
+    if dist:
+        dist[1].destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -418,16 +475,41 @@ def main():
         import shutil
         atexit.register(lambda: shutil.copy("/proc/self/maps", os.environ["LC_MAPS_DUMP"]))
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python3 bench.py --gpus N` (the driver's scaling command) launches its N ranks itself:
+        # one child process per GPU under torch.distributed.run, started before this process
+        # makes any HIP call (never an exec); rank 0's JSON line is relayed
+        raise SystemExit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to "
+                         "report a different GPU count than was asked for")
+    global BACKEND
     local = gpu_index()
     dist = None
     if world > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
+        if os.environ.get("LC_BENCH_PROTOCOL_ONLY"):
+            BACKEND = "gloo"
+        else:
+            ndev = torch.cuda.device_count()
+            if ndev < 1:
+                raise SystemExit("bench.py: no GPU visible")
+            if "LC_BENCH_DEVICE" not in os.environ and ndev < world:
+                # more ranks than GPUs (a 1-GPU box): ranks share devices, which RCCL refuses,
+                # so the bench's own collectives (MAX of the time, SUM of explored) go over gloo
+                local = local % ndev
+                os.environ["LC_BENCH_DEVICE"] = str(local)
+                BACKEND = "gloo"
+            torch.cuda.set_device(local)
         tdist.init_process_group(BACKEND)
         dist = (torch, tdist)
+    if os.environ.get("LC_BENCH_PROTOCOL_ONLY"):
+        # test hook (tests/test_bench_cpu.py): the launch / barrier / max-over-ranks protocol of
+        # this script with no GPU work, so the rank launcher is testable on a CPU-only host
+        return protocol_only(args, rank, world, dist)
 
     def barrier_sync():
         if dist:
@@ -663,7 +745,9 @@ def main():
                 w = float(fx["provenance"]["wall_s"])
                 cpu["whole_history"] = {
                     "value": fx["n_ops"] / w, "configs_per_s": fx["explored"] / w, "wall_s": w,
-                    "gpu_over_cpu": value / (fx["n_ops"] / w),
+                    # this box's GPU rate over an oracle wall time from ANOTHER machine: a
+                    # cross-machine ratio, never to be read as a same-run speedup
+                    "gpu_over_cpu_cross_machine": value / (fx["n_ops"] / w),
                     "same_explored": int(res["explored"][0]) == fx["explored"],
                     "source": f"tests/golden ({fx['provenance'].get('checker', 'oracle')}, build container, "
                               f"{fx['provenance'].get('date', '')}): the whole history, not measured in this run"}

@@ -414,7 +414,18 @@ std::vector<OneOut>& parts_of_thread() {
 
 void encode_trim() { std::vector<OneOut>().swap(parts_of_thread()); }
 
-void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out) {
+// the sink's view of history h of enc (built from enc's concatenated arrays); ninv = scratch
+static HistView view_of(const Encoded& enc, int h, std::vector<int64_t>& ninv) {
+  const int64_t g0 = enc.step_off[h], m = enc.step_off[h + 1] - g0;
+  ninv.resize((size_t)m);
+  for (int64_t s = 0; s < m; ++s) ninv[s] = enc.inv_off[g0 + s + 1] - enc.inv_off[g0 + s];
+  const int64_t q0 = m > 0 ? enc.inv_off[g0] : 0;
+  return HistView{enc.err[h], enc.live_max[h], enc.n_states[h], enc.err[h] ? 0 : m, enc.step_slot.data() + g0,
+                  ninv.data(), enc.inv_slot.data() + q0, enc.inv_a.data() + q0, enc.inv_b.data() + q0,
+                  enc.inv_kind.data() + q0};
+}
+
+void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out, const HistSink* sink) {
   const int n = (int)hs.size();
   out.model = all.model;
   out.n_hist = n;
@@ -426,6 +437,14 @@ void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out
   out.live_max.resize(n);
   out.n_states.resize(n);
   out.n_ops.resize(n);
+  // the sink sees each history straight from `all`; the per-invocation arrays of a history it
+  // takes (its step stream is built) are not copied, as encode() leaves them out
+  std::vector<char> taken(n, 0);
+  if (sink)
+    Pool::get().run(n, all.total_steps() < 100000 ? 1 : 16, [&](int i) {
+      thread_local std::vector<int64_t> ninv;
+      taken[i] = (*sink)(i, view_of(all, hs[i], ninv));
+    });
   std::vector<int64_t> inv_base(n + 1, 0);
   for (int i = 0; i < n; ++i) {
     const int h = hs[i];
@@ -437,7 +456,7 @@ void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out
     const int32_t g0 = all.step_off[h], g1 = all.step_off[h + 1];
     out.step_off[i + 1] = out.step_off[i] + (g1 - g0);
     out.state_off[i + 1] = out.state_off[i] + (all.state_off[h + 1] - all.state_off[h]);
-    inv_base[i + 1] = inv_base[i] + (all.inv_off[g1] - all.inv_off[g0]);
+    inv_base[i + 1] = inv_base[i] + (taken[i] ? 0 : all.inv_off[g1] - all.inv_off[g0]);
   }
   const int64_t ns = out.step_off[n], ni = inv_base[n];
   out.state_val.resize(out.state_off[n]);
@@ -459,7 +478,12 @@ void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out
     std::copy_n(all.step_slot.begin() + g0, m, out.step_slot.begin() + s0);
     std::copy_n(all.step_cmp_idx.begin() + g0, m, out.step_cmp_idx.begin() + s0);
     std::copy_n(all.step_inv_idx.begin() + g0, m, out.step_inv_idx.begin() + s0);
-    const int64_t q0 = all.inv_off[g0], qn = all.inv_off[g0 + m] - q0, o0 = inv_base[i];
+    const int64_t o0 = inv_base[i];
+    if (taken[i]) {
+      for (int64_t s = 0; s < m; ++s) out.inv_off[s0 + s + 1] = o0;
+      return;
+    }
+    const int64_t q0 = all.inv_off[g0], qn = all.inv_off[g0 + m] - q0;
     for (int64_t s = 0; s < m; ++s) out.inv_off[s0 + s + 1] = o0 + (all.inv_off[g0 + s + 1] - q0);
     std::copy_n(all.inv_slot.begin() + q0, qn, out.inv_slot.begin() + o0);
     std::copy_n(all.inv_kind.begin() + q0, qn, out.inv_kind.begin() + o0);
@@ -473,13 +497,7 @@ void sink_encoded(const Encoded& enc, const HistSink& sink) {
   const int64_t ns = enc.total_steps();
   Pool::get().run(enc.n_hist, ns < 100000 ? 1 : 16, [&](int h) {
     thread_local std::vector<int64_t> ninv;
-    const int64_t g0 = enc.step_off[h], m = enc.step_off[h + 1] - g0;
-    ninv.resize((size_t)m);
-    for (int64_t s = 0; s < m; ++s) ninv[s] = enc.inv_off[g0 + s + 1] - enc.inv_off[g0 + s];
-    const int64_t q0 = m > 0 ? enc.inv_off[g0] : 0;
-    sink(h, HistView{enc.err[h], enc.live_max[h], enc.n_states[h], enc.err[h] ? 0 : m, enc.step_slot.data() + g0,
-                     ninv.data(), enc.inv_slot.data() + q0, enc.inv_a.data() + q0, enc.inv_b.data() + q0,
-                     enc.inv_kind.data() + q0});
+    sink(h, view_of(enc, h, ninv));
   });
 }
 

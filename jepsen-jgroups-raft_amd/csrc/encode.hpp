@@ -120,7 +120,8 @@ void encode(int model, int64_t init_value, int n_hist, const int64_t* hist_off,
 // The histories hs of `all` (encoded without a sink: every invocation array kept) as an Encoded
 // of their own, in that order: lc_check(n_gpus > 1) encodes a batch once and gives each shard
 // its histories this way (a parallel copy, no second encode).
-void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out);
+void encoded_subset(const Encoded& all, const std::vector<int>& hs, Encoded& out,
+                    const HistSink* sink = nullptr);
 // sink(h, view) for every history of enc, the views built from enc's arrays (on the pool)
 void sink_encoded(const Encoded& enc, const HistSink& sink);
 // Frees the calling thread's encoder buffers (kept between calls for speed; lc_release).

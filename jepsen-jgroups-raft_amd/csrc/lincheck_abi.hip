@@ -180,6 +180,7 @@ struct lc_plan {
   int wide_grid = 0;  // LC_WIDE_GRID: at most this many workgroups for the HBM tables (0: all resident)
   int wide_watchdog_ms = 20000;  // LC_WIDE_WATCHDOG_MS: a grid barrier's longest wait
   bool wide_force_abort = false;  // LC_WIDE_FORCE_ABORT=1 (tests): the abort word set before launch
+  int wide_stall_hist = -1, wide_stall_wg = -1;  // LC_WIDE_STALL=h:wg (tests): a real barrier stall
   bool wide_pipe = true;  // LC_WIDE_PIPE=0: one step at a time (a grid barrier per popcount layer)
   // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
   // begin / step count / table width, and the queue order
@@ -375,6 +376,10 @@ struct lc_plan {
     if ((e = getenv("LC_WIDE_GRID"))) wide_grid = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_WATCHDOG_MS")) && atoi(e) >= 0) wide_watchdog_ms = atoi(e);
     if ((e = getenv("LC_WIDE_FORCE_ABORT"))) wide_force_abort = atoi(e) != 0;
+    if ((e = getenv("LC_WIDE_STALL")) && strchr(e, ':')) {
+      wide_stall_hist = atoi(e);
+      wide_stall_wg = atoi(strchr(e, ':') + 1);
+    }
     if ((e = getenv("LC_CTAB_MAXW"))) ctab_maxw = std::max(0, std::min(atoi(e), CTAB_LMAX));
     if ((e = getenv("LC_CTAB_PIPE"))) ctab_pipe = atoi(e);
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
@@ -414,6 +419,7 @@ struct lc_plan {
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
     ctab_maxw = CTAB_LMAX, ctab_pipe = 3, wide_watchdog_ms = 20000, wide_force_abort = false;
+    wide_stall_hist = wide_stall_wg = -1;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
     plan_k16 = -1, plan_x = 1.2, plan_kb = 0.45, plan_rot = false, plan_tm = 1.0, plan_lbmin = 12, team_rot = -1, rot_min_lb = 16, rot_chain_lb = 14, rot_chain_min = 14, batch_hist = 600, mid_maxw = 0;
@@ -1862,6 +1868,11 @@ struct lc_plan {
     p.abort = (int32_t*)((char*)d_wbar.p + wide_bar_bytes());
     p.watchdog = (uint64_t)wide_watchdog_ms * 100000ull;
     const int grid = wide_grid > 0 ? std::min(wide_grid, wide_grid_size(p.pipe)) : wide_grid_size(p.pipe);
+    if (wide_stall_hist >= 0 && wide_stall_wg >= 0 && wide_stall_wg < grid) {
+      p.stall = (int32_t*)((char*)d_wbar.p + wide_bar_bytes() + 4);  // (zeroed with the barrier)
+      p.stall_hist = wide_stall_hist;
+      p.stall_wg = wide_stall_wg;
+    }
     if (grid < 1) {
       last_error = "wide kernel: no resident workgroups";
       return LC_E_INTERNAL;
@@ -2076,8 +2087,10 @@ int plan_build(int device, int model, int64_t init_value, int n_hist, const int6
   // the dense step streams are written by the encoder's workers as each history is encoded
   if (!rc) rc = p->dense_prepare(n_hist, hist_off);
   if (!rc && pre) {
-    encoded_subset(*pre, *pre_hs, p->enc);
-    if (p->dense_on) sink_encoded(p->enc, [p](int h, const HistView& v) { return p->dense_sink(h, v); });
+    // the dense sink reads each history from the batch's encoding; the per-invocation arrays
+    // of the histories it takes are not copied (as the single-shard encode leaves them out)
+    const HistSink sink = [p](int h, const HistView& v) { return p->dense_sink(h, v); };
+    encoded_subset(*pre, *pre_hs, p->enc, p->dense_on ? &sink : nullptr);
   } else if (!rc) {
     const HistSink sink = [p](int h, const HistView& v) { return p->dense_sink(h, v); };
     encode(model, init_value, n_hist, hist_off, a, p->enc, p->dense_on ? &sink : nullptr);

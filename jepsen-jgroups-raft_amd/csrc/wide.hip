@@ -63,7 +63,14 @@ __device__ __forceinline__ bool wide_sync(const WideParams& p, int* sAbort) {
     const unsigned grp = blockIdx.x & 7u;
     const unsigned gsize = (nwg - grp + 7u) >> 3;
     const unsigned ngroups = nwg < 8u ? nwg : 8u;
-    if (__hip_atomic_fetch_add(&bar->grp[grp][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+    // (test hook LC_WIDE_STALL: the armed workgroup skips this one arrival, so the barrier
+    // really stalls and the watchdog has to end the launch; null in production)
+    bool skip = false;
+    if (p.stall && (int)blockIdx.x == p.stall_wg && ld_agent(p.stall) == 1) {
+      st_agent(p.stall, 2);
+      skip = true;
+    }
+    if (!skip && __hip_atomic_fetch_add(&bar->grp[grp][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
       st_agent(&bar->grp[grp][0], 0u);
       if (__hip_atomic_fetch_add(&bar->top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1) {
         st_agent(&bar->top, 0u);
@@ -204,6 +211,7 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
   unsigned long long st_fout = 0, st_steps = 0, st_wv = 0, st_wnz = 0;
   for (int i = 0; i < p.n; ++i) {
     const int ns = p.nsteps[i];
+    if (p.stall && i == p.stall_hist && (int)blockIdx.x == p.stall_wg && tid == 0) st_agent(p.stall, 1);
     uint64_t* const T0 = p.tab;
     uint64_t* const T1 = p.tab + p.tab_words;
     auto tab = [&](int t) { return (t & 1) ? T1 : T0; };
@@ -328,15 +336,15 @@ __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
     __syncthreads();
     if (lane == 0 && expl) atomicAdd(&sRed, expl);
     __syncthreads();
-    if (tid == 0) {
-      if (sRed) atomicAdd(&p.explored[i], sRed);
-      if (blockIdx.x == 0) {
-        p.status[i] = fail_t >= 0 ? ST_INVALID : ST_VALID;
-        p.fail_step[i] = fail_t;
-      }
-    }
+    if (tid == 0 && sRed) atomicAdd(&p.explored[i], sRed);
     // (the next history's first store is to T1[0]: every workgroup is past this one's reads)
     if (!wide_sync(p, &sAbort)) break;
+    // the verdict only once every workgroup has added its explored count (a workgroup whose
+    // watchdog fires at this barrier leaves without it, and then the history stays unfinished)
+    if (blockIdx.x == 0 && tid == 0) {
+      p.status[i] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      p.fail_step[i] = fail_t;
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
     st_fout += __shfl_down(st_fout, off, 64);
@@ -416,6 +424,7 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
   unsigned long long st_fout = 0, st_steps = 0, st_wv = 0, st_wnz = 0;
   for (int i = 0; i < p.n && !sAbort; ++i) {
     const int ns = p.nsteps[i];
+    if (p.stall && i == p.stall_hist && (int)blockIdx.x == p.stall_wg && tid == 0) st_agent(p.stall, 1);
     uint64_t* const T0 = p.tab;
     uint64_t* const T1 = p.tab + p.tab_words;
     auto tab = [&](int t) { return (t & 1) ? T1 : T0; };
@@ -580,14 +589,14 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
     __syncthreads();
     if (lane == 0 && expl) atomicAdd(&sRed, expl);
     __syncthreads();
-    if (tid == 0) {
-      if (sRed) atomicAdd(&p.explored[i], sRed);
-      if (blockIdx.x == 0) {
-        p.status[i] = fail_t >= 0 ? ST_INVALID : ST_VALID;
-        p.fail_step[i] = fail_t;
-      }
-    }
+    if (tid == 0 && sRed) atomicAdd(&p.explored[i], sRed);
     if (!wide_sync(p, &sAbort)) break;
+    // the verdict only once every workgroup has added its explored count (a workgroup whose
+    // watchdog fires at this barrier leaves without it, and then the history stays unfinished)
+    if (blockIdx.x == 0 && tid == 0) {
+      p.status[i] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      p.fail_step[i] = fail_t;
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
     st_fout += __shfl_down(st_fout, off, 64);

@@ -48,6 +48,10 @@ struct WideParams {
   uint32_t* anyv;             // pipelined: per history, bit t = some X of step t was nonzero (zeroed)
   uint64_t watchdog;          // s_memrealtime ticks (100 MHz) a grid barrier may wait before *abort
   const int64_t* anyv_off;    // [n] word offset of each history's bits (ns / 32 + 1 words)
+  // test hook (LC_WIDE_STALL=h:wg, tests only; stall = null otherwise): workgroup stall_wg
+  // arms *stall as it starts history stall_hist and then skips its next barrier arrival
+  int32_t* stall;
+  int32_t stall_hist, stall_wg;
 };
 
 hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream);

@@ -287,6 +287,27 @@ def gen_config(name: str, key0: int = 0, scale: float = 1.0) -> History:
     return gen_register_keys(n_keys, ops, c["clients"], c["p_info"], config_id=cid, key0=key0)
 
 
+def perturb_read(h: History, at_frac: float, model: str = "cas-register", seed: int = 0) -> History:
+    """A copy of single history h with ONE :ok read changed: the first :ok read completion at or
+    after entry at_frac * n whose value is a scalar. A register read v becomes (v + 1 + r) % 5
+    (another value of the generator's domain), a counter read v + 1 + r, r ~ U{0..3} from seed.
+    The full-size invalid fixtures (tests/golden/pin_wide.py) stop the search mid-history."""
+    from .history import from_columns
+    t, f, vf = np.asarray(h.type), np.asarray(h.f), np.asarray(h.vflags)
+    start = int(at_frac * h.n)
+    cand = np.nonzero((t[start:] == T_OK) & (f[start:] == F_READ) & (vf[start:] == V_SCALAR))[0]
+    if not len(cand):
+        raise ValueError("no :ok scalar read after the requested point")
+    j = start + int(cand[0])
+    r = 1 + int(np.random.default_rng(seed).integers(0, 4))
+    v0 = np.array(h.v0, copy=True)
+    v0[j] = (v0[j] + r) % 5 if model == "cas-register" else v0[j] + r
+    out = from_columns(np.array(h.index, copy=True), np.array(h.process, copy=True), t.copy(),
+                       f.copy(), v0, np.array(h.v1, copy=True), vf.copy())
+    out.keys = list(getattr(h, "keys", None) or [0])
+    return out
+
+
 def truncate(h: History, m: int) -> History:
     """Prefix of the first m entries of a single history (bounded CPU-baseline samples)."""
     from .history import from_columns

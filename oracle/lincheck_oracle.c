@@ -374,7 +374,7 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
   if (!cset_init(&S, 1024) || !cset_init2(&O, 1024, track)) { set_err(out, -3, "out of memory"); rc = -3; }
   cfg c0 = {0, model_kind == OR_MODEL_LEADER ? 0 : init_value, model_kind == OR_MODEL_CAS_REGISTER ? 1 : 0, -1};
   if (model_kind == OR_MODEL_CAS_REGISTER) c0.value = 0; /* (cas-register) starts at nil */
-  if (!rc) cvec_push(&F, &c0);
+  if (!rc && !cvec_push(&F, &c0)) rc = -3;
   out->max_frontier = 1;
   int64_t last_ok = -1;
 
@@ -405,10 +405,10 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
         if (ins < 0) { rc = -3; break; }
         if (ins) {
           if (track) O.pos[at] = OUT.n;
-          cvec_push(&OUT, &c);
+          if (!cvec_push(&OUT, &c)) { rc = -3; break; }
         }
-      } else {
-        cvec_push(&L, &c);
+      } else if (!cvec_push(&L, &c)) {
+        rc = -3; break;
       }
     }
     while (L.n && !rc) {
@@ -438,12 +438,12 @@ int32_t oracle_check(int32_t model_kind, int64_t init_value, int64_t n, const in
             if (ins2 < 0) { rc = -3; break; }
             if (ins2) {
               if (track) O.pos[at] = OUT.n;
-              cvec_push(&OUT, &r);
+              if (!cvec_push(&OUT, &r)) { rc = -3; break; }
             } else if (track) {
               OUT.v[O.pos[at]].last = r.last; /* carried through before: the closure's is newer */
             }
-          } else {
-            cvec_push(&NL, &c2);
+          } else if (!cvec_push(&NL, &c2)) {
+            rc = -3; break;
           }
           if (max_configs > 0 && (S.count > max_configs || O.count > max_configs)) {
             set_err(out, -7, "max_configs exceeded");

@@ -45,3 +45,35 @@ def test_golden_fixture_for_single_history_lines(bench, workload):
     fx = bench.golden_fixture(workload)
     assert fx is not None and fx["explored"] > 0 and fx["provenance"]["wall_s"] > 0
     assert bench.golden_fixture("c3") is None
+
+
+def _run_bench(argv, env_extra, timeout=240):
+    import subprocess
+    import sys
+    env = dict(os.environ, **env_extra)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        if k not in env_extra:
+            env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + argv, capture_output=True,
+                          text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_launches_n_ranks(n):
+    """plain `python3 bench.py --gpus N` (the driver's scaling command) starts
+    N ranks itself under torch.distributed.run and relays rank 0's one JSON line. The GPU work is
+    skipped by the LC_BENCH_PROTOCOL_ONLY hook so the launcher runs here (gloo, no GPU)."""
+    import json
+    r = _run_bench(["--gpus", str(n), "--steps", "2", "--warmup", "1"], {"LC_BENCH_PROTOCOL_ONLY": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["ranks_seen"] == n and out["steps"] == 2
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    """Under an external launcher, --gpus must equal WORLD_SIZE (no silent one-rank runs)."""
+    r = _run_bench(["--gpus", "8", "--steps", "1", "--warmup", "0"],
+                   {"WORLD_SIZE": "1", "RANK": "0", "LC_BENCH_PROTOCOL_ONLY": "1"}, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

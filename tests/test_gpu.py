@@ -1051,6 +1051,26 @@ def test_gpu_bench_two_ranks_one_gpu(workload, tmp_path):
         assert out["verdict"]["bounds_ok"] is True
 
 
+def test_gpu_bench_gpus_2_launches_its_ranks():
+    """plain `python3 bench.py --gpus 2` (no external launcher, as the driver
+    runs it) spawns 2 ranks itself; on a 1-GPU box they share cuda:0 and the bench's collectives
+    go over gloo. One JSON line with n_gpus = 2 and every key counted once."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LC_BENCH_DEVICE", "LC_BENCH_BACKEND")}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu", "--scale", "0.2", "--e2e-reps", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["histories"] == 200
+    assert out["verdicts"]["0"] == 0
+
+
 # ---- closure tables in HBM (wide.hip, DESIGN §3.10): live width 25..35 -------------------
 
 @pytest.mark.parametrize("pipe,grid", [("1", "0"), ("0", "0"), ("1", "8")])
@@ -1192,6 +1212,43 @@ def test_gpu_wide_watchdog_abort_is_unknown(monkeypatch):
     monkeypatch.delenv("LC_WIDE_FORCE_ABORT")
     g2 = _lib.check(1, 0, h)  # the next call runs normally
     assert int(g2["valid"][last]) == oracle.check_one("cas-register", h.select([last]))["valid"]
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_gpu_wide_watchdog_real_stall(pipe, monkeypatch):
+    """VERDICT r4 item 8 / ADVICE r4: a grid barrier that REALLY stalls. Workgroup 3 skips its
+    barrier arrival at the start of the second wide history (LC_WIDE_STALL=1:3), so no workgroup
+    can pass that barrier and the 200 ms watchdog (wide.hip wide_sync) ends the launch. The first
+    wide history finished before the stall: its verdict AND explored count equal the oracle's
+    (the status is written only after every workgroup added its count). The stalled history and
+    the ones after it are :unknown (LC_H_ABORTED), the narrow histories keep their answers, and
+    the next call runs normally."""
+    monkeypatch.setenv("LC_WIDE_MINW", "12")
+    monkeypatch.setenv("LC_WIDE_PIPE", pipe)
+    monkeypatch.setenv("LC_WIDE_WATCHDOG_MS", "200")
+    monkeypatch.setenv("LC_WIDE_STALL", "1:3")
+    narrow = [synth.gen_register(200, 4, 0.01, 56200 + t, invalid=(t % 2 == 1)) for t in range(6)]
+    wide = [synth.gen_register(400, 16, 0.01, 56300 + t, n_crashed=2, invalid=(t == 0)) for t in range(3)]
+    h = H.concat(narrow + wide)
+    nw = len(narrow)
+    assert all(_live_width(h, k) >= 12 for k in range(nw, h.n_hist))
+    assert all(_live_width(h, k) < 12 for k in range(nw))
+    exp = oracle.check_many("cas-register", h)
+    g = _lib.check(1, 0, h)
+    assert _lib.check_stats()["wide_histories"] == 3
+    for k in range(nw):
+        _cmp(g, exp[k], k, "beside a stalled wide launch")
+    decided = [k for k in range(nw, h.n_hist) if int(g["err"][k]) != -8]
+    aborted = [k for k in range(nw, h.n_hist) if int(g["err"][k]) == -8]
+    assert len(decided) == 1 and len(aborted) == 2, (decided, aborted, g["err"][nw:])
+    for k in decided:
+        _cmp(g, exp[k], k, "finished before the stall")
+    for k in aborted:
+        assert int(g["valid"][k]) == 2
+    monkeypatch.delenv("LC_WIDE_STALL")
+    g2 = _lib.check(1, 0, h)  # a clean next call
+    for k in range(h.n_hist):
+        _cmp(g2, exp[k], k, "after the stall")
 
 
 def test_gpu_fuzz_register_and_counter_vs_oracle():

@@ -247,3 +247,21 @@ def test_counter_fixtures_match_generator(name):
     if name == "c2c":
         r = oracle.check_one("counter", h)
         assert (r["valid"], r["explored"], r["fail_idx"]) == (gold["valid"], gold["explored"], gold["fail_idx"])
+
+
+@pytest.mark.parametrize("name", ["ramp13", "ramp14", "ramp16", "ramp13x50", "c4x15", "c5xx2"])
+def test_wide_fixtures_match_generator(name):
+    """tests/golden/wide_<name>_oracle.json (tests/golden/pin_wide.py: real wide frontiers and
+    full-size invalid runs) was made from this generator's history."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import pin_wide
+    p = pin_wide.path_of(name)
+    if not os.path.exists(p):
+        pytest.skip(f"{name} not pinned")
+    gold = json.load(open(p))
+    h = pin_wide.GEN[name][2]()
+    assert (h.n, h.n_ops()) == (gold["n_entries"], gold["n_ops"])
+    assert pin_wide.digest(h) == gold["digest"]
+    assert gold["err_code"] == 0 and gold["valid"] in (0, 1)
+    if name.endswith(("x50", "x15", "x2")):
+        assert gold["valid"] == 0 and gold["fail_idx"] > 0  # a mid-history stop
