@@ -584,6 +584,11 @@ struct lc_plan {
     for (int h = 0; h < n; ++h) sbeg[h] = mul * (hist_off[h] - hist_off[0]) + h;
     return 0;
   }
+  // lc_failure_configs on the HBM tables: run_wide stops each history after wide_stop steps (-1:
+  // all), and records the tables' layout of its last launch
+  int wide_stop = -1;
+  bool wide_last_ranked = false, wide_ran = false;
+  int wide_last_hm = 0;
   bool keep_inv_arrays = false;  // lc_failure_configs: its grid re-run needs every history's
   // returns true when h's step stream was built (its invocation arrays are then not needed)
   bool dense_sink(int h, const HistView& v) {
@@ -1794,6 +1799,159 @@ struct lc_plan {
     return 0;
   }
 
+  // lc_failure_configs for history 0 on the HBM tables: the frontier before
+  // its failing RETURN t and every config's :last-op, from the tables themselves. Knossos's
+  // per-config :last-op: config (m, v) of that frontier was either produced by step
+  // t-1's closure linearizing t-1's returning op j (then that op is its last), or carried through
+  // that return from (m + j, v) in step t-1's frontier (then it keeps that config's). The closure
+  // produced (m + j, v) iff some state u of the FINAL step t-1 table at mask m steps to v under
+  // j's op (T_j(B[m]): R at masks holding j, dense.hip §3.1), so the walk needs one word per
+  // config per step back. A run stopped after step S - 1 (wide_stop = S) leaves the final tables of
+  // steps S - 1 and S - 2 in place; deeper walks re-run to an earlier stop. Returns
+  // LC_E_CONFIGS when the frontier outgrows the dump (the report is then unavailable).
+  struct RepCfg {
+    uint64_t mask;
+    int state, last_step;  // state id (0 = nil); the step whose closure produced it (-1: initial)
+  };
+  int wide_report(int t_fail, std::vector<RepCfg>& out) {
+    out.clear();
+    if (t_fail <= 0) {  // the failing RETURN is the first: its frontier is the initial config
+      out.push_back({0ull, 0, -1});
+      return 0;
+    }
+    // per step: live slots, returning slot, its op's (amask, bmask) (wide_sink's stream)
+    const std::vector<uint32_t>& ws = wide_streams[0];
+    std::vector<uint64_t> live_s;
+    std::vector<int> j_s;
+    std::vector<uint32_t> am_s, bm_s;
+    {
+      uint32_t am[64] = {0}, bm[64] = {0};
+      size_t q = 0;
+      while (q + 2 < ws.size() && (int)live_s.size() < t_fail) {
+        const uint64_t live = (uint64_t)ws[q] | ((uint64_t)ws[q + 1] << 31);
+        const int j = (int)ws[q + 2];
+        q += 3;
+        for (; q < ws.size() && (ws[q] & DENSE_OPW); ++q) {
+          const uint32_t w = ws[q], sl = w & 63u;
+          am[sl] = (w >> 8) & 0xffu, bm[sl] = (w >> 16) & 0xffu;
+        }
+        live_s.push_back(live), j_s.push_back(j), am_s.push_back(am[j]), bm_s.push_back(bm[j]);
+      }
+      if ((int)live_s.size() < t_fail) {
+        last_error = "failure configs: the wide step stream ends before the failing step";
+        return LC_E_INTERNAL;
+      }
+    }
+    auto run_to = [&](int stop) -> int {
+      wide_stop = stop;
+      wide_ran = false;
+      const int rc = run();
+      wide_stop = -1;
+      if (rc) return rc;
+      if (!wide_ran) {
+        last_error = "failure configs: the history did not run on the HBM tables";
+        return LC_E_CONFIGS;
+      }
+      return 0;
+    };
+    int rc = run_to(t_fail);
+    if (rc) return rc;
+    const int64_t tw = (int64_t)1 << wide_last_hm;
+    auto table_of = [&](int s) { return d_wtab.as<uint64_t>() + ((s & 1) ? tw : 0); };
+    WideDumpParams d{};
+    d.ranked = wide_last_ranked ? 1 : 0;
+    d.Hm = wide_last_hm;
+    // the dump: the frontier before step t_fail
+    const int64_t cap = (int64_t)1 << 22;
+    DevArray d_masks, d_states, d_cnt;
+    HIP_TRY(d_masks.ensure((size_t)cap * 8));
+    HIP_TRY(d_states.ensure((size_t)cap));
+    HIP_TRY(d_cnt.ensure(8));
+    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 8, stream));
+    d.tab = table_of(t_fail - 1);
+    d.jp = j_s[t_fail - 1];
+    d.lv = live_s[t_fail - 1] & ~(1ull << d.jp);
+    d.cap = cap;
+    d.masks = d_masks.as<uint64_t>();
+    d.states = d_states.as<uint8_t>();
+    d.count = d_cnt.as<unsigned long long>();
+    HIP_TRY(launch_wide_dump(d, stream));
+    unsigned long long cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, d_cnt.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if ((int64_t)cnt > cap) {
+      last_error = "failure configs unavailable: the pre-failure frontier holds " + std::to_string(cnt) +
+                   " configs, more than the dump's " + std::to_string(cap);
+      return LC_E_CONFIGS;
+    }
+    std::vector<uint64_t> masks(cnt);
+    std::vector<uint8_t> states(cnt);
+    HIP_TRY(hipMemcpy(masks.data(), d_masks.p, cnt * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(states.data(), d_states.p, cnt, hipMemcpyDeviceToHost));
+    out.resize(cnt);
+    std::vector<uint64_t> cur(cnt);
+    std::vector<int> open;
+    for (size_t i = 0; i < cnt; ++i) {
+      out[i] = {masks[i], (int)states[i], -2};
+      cur[i] = masks[i];
+      open.push_back((int)i);
+    }
+    // the walk, one step back per round: tables of steps S - 1, S - 2 are in place
+    int S = t_fail;
+    DevArray d_hw, d_words;
+    std::vector<uint32_t> hw;
+    std::vector<uint64_t> words;
+    for (int st = t_fail - 1; st >= 0 && !open.empty(); --st) {
+      if (st < S - 2) {
+        S = st + 1;
+        if ((rc = run_to(S))) return rc;
+      }
+      hw.resize(open.size());
+      for (size_t k = 0; k < open.size(); ++k) hw[k] = (uint32_t)(cur[open[k]] >> 3);
+      HIP_TRY(d_hw.ensure(hw.size() * 4));
+      HIP_TRY(d_words.ensure(hw.size() * 8));
+      HIP_TRY(hipMemcpy(d_hw.p, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+      d.tab = table_of(st);
+      HIP_TRY(launch_wide_gather(d, d_hw.as<uint32_t>(), d_words.as<uint64_t>(), (int)hw.size(), stream));
+      words.resize(hw.size());
+      HIP_TRY(hipMemcpyAsync(words.data(), d_words.p, words.size() * 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      const uint32_t am = am_s[st], bm = bm_s[st];
+      const int j = j_s[st];
+      std::vector<int> still;
+      for (size_t k = 0; k < open.size(); ++k) {
+        const int i = open[k];
+        const int pm = (int)(cur[i] & 7u), v = out[i].state;
+        auto has = [&](int u) { return (words[k] >> (8 * u + pm)) & 1u; };
+        bool produced = false;  // CASRegister.step of j's op from some state at mask cur (a6)
+        if (am == 0) {
+          produced = false;  // names a value the register never holds
+        } else if (bm) {
+          const int dst = __builtin_ctz(bm);
+          if (v == dst) {
+            if (am == 0xffu) {  // write: from any state
+              for (int u = 0; u < 8 && !produced; ++u) produced = has(u);
+            } else {  // cas a -> dst
+              produced = has(__builtin_ctz(am));
+            }
+          }
+        } else if (am == 0xffu) {
+          produced = has(v);  // read nil: every state stays
+        } else {
+          produced = v == __builtin_ctz(am) && has(v);  // read a
+        }
+        if (produced) out[i].last_step = st;
+        else cur[i] |= 1ull << j, still.push_back(i);
+      }
+      open.swap(still);
+    }
+    if (!open.empty()) {
+      last_error = "failure configs: a config's :last-op walk reached the history's start";
+      return LC_E_CONFIGS;
+    }
+    return 0;
+  }
+
   // The wide histories (tables in HBM), one persistent launch over the whole GPU, one history
   // after another. `ran` stays false when the two tables do not fit the device (they then take
   // the grid kernel, as before).
@@ -1807,7 +1965,7 @@ struct lc_plan {
     for (int i = 0; i < nwd; ++i) {
       const int h = dense_wd[i];
       sbeg[i] = (int64_t)words.size();
-      nst[i] = enc.n_steps(h);
+      nst[i] = wide_stop >= 0 ? std::min(enc.n_steps(h), wide_stop) : enc.n_steps(h);
       lmx[i] = (int8_t)enc.live_max[h];
       lmax = std::max(lmax, (int)enc.live_max[h]);
       words.insert(words.end(), wide_streams[h].begin(), wide_streams[h].end());
@@ -1853,6 +2011,7 @@ struct lc_plan {
     p.lmax = (const int8_t*)((char*)d_wmeta.p + 2 * m_sb + m_ns);
     // (the one-step kernel's prefix tables stop at WIDE_NOPIPE_LMAX: wider tables always pipeline)
     p.pipe = wide_pipe || lmax > WIDE_NOPIPE_LMAX ? 1 : 0;
+    wide_last_ranked = p.pipe != 0, wide_last_hm = std::max(0, lmax - 3);
     p.stream = d_wstream.as<uint32_t>();
     p.words = d_dwords.as<uint32_t>();
     p.tab = d_wtab.as<uint64_t>();
@@ -1929,6 +2088,7 @@ struct lc_plan {
               "words visited %llu, stored nonzero %llu (%.2f %%)\n", nwd, std::max(0, lmax - 3), t, ss[1], ss[0], ss[2],
               ss[3], 100.0 * (double)ss[3] / (double)std::max(1ull, ss[2]));
     ran = true;
+    wide_ran = true;
     return 0;
   }
 
@@ -2559,12 +2719,69 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
   // per-config :last-op; its grid-kernel re-run can take minutes at these widths (the crash
   // ramp's width-27 history did not finish in 3), so the report stops here unless asked
   // (LC_WIDE_CONFIGS=1). The verdict, failing op and explored count stand.
-  if (p->enc.live_max[0] > DENSE_WIDE_LMAX && p->enc.live_max[0] <= WIDE_LMAX &&
-      p->enc.model == LC_MODEL_CAS_REGISTER &&
-      !(getenv("LC_WIDE_CONFIGS") && atoi(getenv("LC_WIDE_CONFIGS")) != 0)) {
-    set_err(err, err_len, "failure configs unavailable: %d live slots (> %d: decided on the HBM tables)",
-            p->enc.live_max[0], DENSE_WIDE_LMAX);
-    return LC_E_CONFIGS;
+  const Encoded& en = p->enc;
+  // the pending ops at the failing RETURN, by slot (replayed slot assignments)
+  int64_t slot_inv[64];
+  for (int s = 0; s < 64; ++s) slot_inv[s] = -1;
+  for (int t = 0; t <= t_fail; ++t) {
+    const int64_t g = en.step_off[0] + t;
+    if (t > 0) slot_inv[en.step_slot[g - 1]] = -1;
+    for (int64_t q = en.inv_off[g]; q < en.inv_off[g + 1]; ++q) slot_inv[en.inv_slot[q]] = en.inv_index[q];
+  }
+  auto last_of_step = [&](int s) -> int64_t {  // :ok completion of step s's returning op
+    return s >= 0 ? en.step_cmp_idx[en.step_off[0] + s] : -1;
+  };
+  // emit: configs (state id, slot mask, producing step) sorted by (state, mask), the first k
+  auto emit = [&](std::vector<lc_plan::RepCfg>& all, int mask_bits) -> int32_t {
+    std::sort(all.begin(), all.end(), [](const lc_plan::RepCfg& x, const lc_plan::RepCfg& y) {
+      return x.state != y.state ? x.state < y.state : x.mask < y.mask;
+    });
+    int np = 0;
+    for (int s = 0; s < 64; ++s)
+      if (slot_inv[s] >= 0) {
+        if (pending) pending[np] = slot_inv[s];
+        ++np;
+      }
+    if (n_pending) *n_pending = np;
+    int64_t newest = -1;
+    for (const auto& c : all) newest = std::max(newest, last_of_step(c.last_step));
+    if (out_last_op) *out_last_op = newest;
+    int out = 0;
+    for (const auto& c : all) {
+      if (out >= k) break;
+      int64_t val = 0;
+      int8_t nil = 0;
+      if (c.state == 0) nil = 1;
+      else val = en.state_val[en.state_off[0] + c.state - 1];
+      int nl = 0;
+      for (int s = 0; s < mask_bits; ++s)
+        if ((c.mask >> s) & 1) {
+          if (linearized) linearized[(size_t)out * 64 + nl] = slot_inv[s];
+          ++nl;
+        }
+      if (state) state[out] = val;
+      if (is_nil) is_nil[out] = nil;
+      if (n_lin) n_lin[out] = nl;
+      if (last_op) last_op[out] = last_of_step(c.last_step);
+      ++out;
+    }
+    if (n_out) *n_out = out;
+    return 0;
+  };
+  // a history wider than the LDS tables was decided on the HBM tables (wide.hip): its report
+  // comes from the tables (a stopped re-run, the frontier dumped, each config's :last-op walked
+  // back), not from the grid kernel, which takes minutes at these widths (LC_WIDE_CONFIGS=0
+  // forces the grid-kernel re-run, for tests)
+  // (the route is the check's own: LC_WIDE_MINW sends narrower histories there too, for tests)
+  if (p->enc.model == LC_MODEL_CAS_REGISTER && !p->dense_wd.empty() &&
+      !(getenv("LC_WIDE_CONFIGS") && atoi(getenv("LC_WIDE_CONFIGS")) == 0)) {
+    std::vector<lc_plan::RepCfg> all;
+    rc = p->wide_report(t_fail, all);
+    if (rc) {
+      set_err(err, err_len, "%s", p->last_error.c_str());
+      return rc;
+    }
+    return emit(all, WIDE_LMAX);
   }
   // stop before the failing RETURN: the frontier it saw stays in flist (the grid kernel: the
   // dense tables keep no config lists), each config tagged with the step that emitted it. A key
@@ -2591,22 +2808,6 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
             "grid kernel's capacity (status %d)", hist, p->status[0]);
     return LC_E_CONFIGS;
   }
-  // replay slot assignments to step t_fail
-  const Encoded& en = p->enc;
-  int64_t slot_inv[64];
-  for (int s = 0; s < 64; ++s) slot_inv[s] = -1;
-  for (int t = 0; t <= t_fail; ++t) {
-    const int64_t g = en.step_off[0] + t;
-    if (t > 0) slot_inv[en.step_slot[g - 1]] = -1;
-    for (int64_t q = en.inv_off[g]; q < en.inv_off[g + 1]; ++q) slot_inv[en.inv_slot[q]] = en.inv_index[q];
-  }
-  int np = 0;
-  for (int s = 0; s < 64; ++s)
-    if (slot_inv[s] >= 0) {
-      if (pending) pending[np] = slot_inv[s];
-      ++np;
-    }
-  if (n_pending) *n_pending = np;
   // read the frontier lists of buffer (t_fail & 1): (config, tag) entries; per config the most
   // recent tag wins (age = steps since the emitting closure; a carried config is at most
   // width-many RETURNs old, < 64)
@@ -2639,6 +2840,20 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
   });
   all.erase(std::unique(all.begin(), all.end(), [](const Cfg& x, const Cfg& y) { return x.cfg == y.cfg; }),
             all.end());
+  if (L.model == LC_MODEL_CAS_REGISTER) {
+    const uint64_t sm = (1ull << bt.state_bits) - 1;
+    std::vector<lc_plan::RepCfg> rep;
+    rep.reserve(all.size());
+    for (const Cfg& c : all)
+      rep.push_back({c.cfg & ((1ull << bt.mask_bits) - 1), (int)((c.cfg >> bt.mask_bits) & sm),
+                     t_fail == 0 ? -1 : t_fail - 1 - c.age});
+    return emit(rep, bt.mask_bits);
+  }
+  // counter / leader: the value is the config's second word
+  {
+    std::vector<lc_plan::RepCfg> none;
+    emit(none, 0);  // the pending ops and an empty output, then the configs below
+  }
   auto last_index = [&](int age) -> int64_t {  // :ok completion of the emitting step's op
     const int s = t_fail - 1 - age;
     return s >= 0 ? en.step_cmp_idx[en.step_off[0] + s] : -1;
@@ -2649,22 +2864,14 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
   int out = 0;
   for (const Cfg& c : all) {
     if (out >= k) break;
-    int64_t val = c.val;
-    int8_t nil = 0;
-    if (L.model == LC_MODEL_CAS_REGISTER) {
-      const uint64_t sm = (1ull << bt.state_bits) - 1;
-      const int64_t id = (int64_t)((c.cfg >> bt.mask_bits) & sm);
-      if (id == 0) nil = 1;
-      else val = en.state_val[en.state_off[0] + id - 1];
-    }
     int nl = 0;
     for (int s = 0; s < bt.mask_bits; ++s)
       if ((c.cfg >> s) & 1) {
         if (linearized) linearized[(size_t)out * 64 + nl] = slot_inv[s];
         ++nl;
       }
-    if (state) state[out] = val;
-    if (is_nil) is_nil[out] = nil;
+    if (state) state[out] = c.val;
+    if (is_nil) is_nil[out] = 0;
     if (n_lin) n_lin[out] = nl;
     if (last_op) last_op[out] = t_fail == 0 ? -1 : last_index(c.age);
     ++out;

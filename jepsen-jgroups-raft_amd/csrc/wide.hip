@@ -23,6 +23,8 @@
 #include "search.hpp"
 #include "wide.hpp"
 
+#include <algorithm>
+
 namespace lc {
 namespace {
 
@@ -609,6 +611,79 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
   if (lane == 0 && st_wnz) atomicAdd(&p.stats[3], st_wnz);
 }
 
+// ---- failure reports from the tables (lc_failure_configs). After a run that
+// stopped after step t - 1 (WideParams nsteps = the failing step t), tab(t - 1) holds step t - 1's
+// whole table; the frontier the failing RETURN saw is that table read through t - 1's returning
+// slot jp (the X of step t; its fresh slots are not live yet), dumped here config by config.
+__device__ __forceinline__ uint32_t dump_index(uint32_t w, const WideDumpParams& d, const uint32_t* bin,
+                                               const uint32_t* off) {
+  return d.ranked ? off[__popc(w)] + colex_rank(w, bin) : w;
+}
+
+__global__ void __launch_bounds__(256) wide_dump_kernel(WideDumpParams d) {
+  __shared__ uint32_t sBin[WB * WB];
+  __shared__ uint32_t sOff[WH + 2];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < WB * WB; i += 256) {
+    const int n = i / WB, k = i % WB;
+    uint64_t c = 0;
+    if (k <= n) {
+      c = 1;
+      for (int q = 1; q <= k; ++q) c = c * (uint64_t)(n - k + q) / (uint64_t)q;
+    }
+    sBin[i] = (uint32_t)c;
+  }
+  __syncthreads();
+  if (tid <= WH + 1) {
+    uint32_t o = 0;
+    for (int r = 0; r < tid && r <= d.Hm; ++r) o += sBin[d.Hm * WB + r];
+    sOff[tid] = o;
+  }
+  __syncthreads();
+  const int Lf = d.lv ? 64 - __clzll((long long)d.lv) : 0;
+  const int64_t nwt = (int64_t)1 << (Lf > 3 ? Lf - 3 : 0);
+  for (int64_t w = (int64_t)blockIdx.x * 256 + tid; w < nwt; w += (int64_t)gridDim.x * 256) {
+    if ((uint64_t)w & ~(d.lv >> 3)) continue;
+    const uint32_t wr = d.jp >= 3 ? (uint32_t)w | (1u << (d.jp - 3)) : (uint32_t)w;
+    uint64_t X = HbmTab::ld(&d.tab[dump_index(wr, d, sBin, sOff)]);
+    if (d.jp < 3) X = (X & ~keep64(d.jp)) >> (1 << d.jp);
+    if (!X) continue;
+    unsigned long long at = atomicAdd(d.count, (unsigned long long)__popcll(X));
+    for (; X; X &= X - 1, ++at) {
+      const int b = __builtin_ctzll(X);
+      if ((int64_t)at < d.cap) {
+        d.masks[at] = ((uint64_t)w << 3) | (uint64_t)(b & 7);
+        d.states[at] = (uint8_t)(b >> 3);
+      }
+    }
+  }
+}
+
+// out[i] = table word at the hi-bit word hw[i] (the ranked or natural index, as dump_index)
+__global__ void __launch_bounds__(256) wide_gather_kernel(WideDumpParams d, const uint32_t* hw, uint64_t* out, int n) {
+  __shared__ uint32_t sBin[WB * WB];
+  __shared__ uint32_t sOff[WH + 2];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < WB * WB; i += 256) {
+    const int nn = i / WB, k = i % WB;
+    uint64_t c = 0;
+    if (k <= nn) {
+      c = 1;
+      for (int q = 1; q <= k; ++q) c = c * (uint64_t)(nn - k + q) / (uint64_t)q;
+    }
+    sBin[i] = (uint32_t)c;
+  }
+  __syncthreads();
+  if (tid <= WH + 1) {
+    uint32_t o = 0;
+    for (int r = 0; r < tid && r <= d.Hm; ++r) o += sBin[d.Hm * WB + r];
+    sOff[tid] = o;
+  }
+  __syncthreads();
+  for (int i = blockIdx.x * 256 + tid; i < n; i += gridDim.x * 256)
+    out[i] = HbmTab::ld(&d.tab[dump_index(hw[i], d, sBin, sOff)]);
+}
+
 }  // namespace
 
 int wide_grid_size(bool pipe) {
@@ -628,6 +703,17 @@ int wide_grid_size(bool pipe) {
 }
 
 size_t wide_bar_bytes() { return sizeof(WideBar); }
+
+hipError_t launch_wide_dump(const WideDumpParams& d, hipStream_t stream) {
+  hipLaunchKernelGGL(wide_dump_kernel, dim3(1024), dim3(256), 0, stream, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_gather(const WideDumpParams& d, const uint32_t* hw, uint64_t* out, int n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wide_gather_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, d, hw, out, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream) {
   WideParams q = p;

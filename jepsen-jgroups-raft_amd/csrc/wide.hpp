@@ -54,7 +54,25 @@ struct WideParams {
   int32_t stall_hist, stall_wg;
 };
 
+// failure reports (lc_failure_configs): the frontier before step t, read from tab = step t - 1's
+// table through its returning slot jp, over the post-return live slots lv; configs (mask, state)
+// in any order, at most cap of them, *count = all of them
+struct WideDumpParams {
+  const uint64_t* tab;
+  int32_t ranked;  // the pipelined kernel's layout (colex_rank), else word w at index w
+  int32_t Hm;      // the table holds 2^Hm words
+  uint64_t lv;
+  int32_t jp;
+  int64_t cap;
+  uint64_t* masks;
+  uint8_t* states;
+  unsigned long long* count;
+};
+
 hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream);
+hipError_t launch_wide_dump(const WideDumpParams& d, hipStream_t stream);
+// out[i] = the word of tab (as d: layout, Hm) at hi-bit word hw[i]
+hipError_t launch_wide_gather(const WideDumpParams& d, const uint32_t* hw, uint64_t* out, int n, hipStream_t stream);
 int wide_grid_size(bool pipe);
 size_t wide_bar_bytes();
 

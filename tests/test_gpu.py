@@ -1157,14 +1157,57 @@ def test_gpu_wide_tables_past_the_tile_teams():
         assert e["valid"] == (0 if bad else 1)
         _cmp(g, e, 0, f"wide w={w}")
         assert int(g["explored"][0]) == oracle.check_one("cas-register", base)["explored"]
-        if bad:  # no failure report from the HBM tables: LC_E_CONFIGS, the verdict stands
-            with pytest.raises(_lib.LincheckError, match="unavailable"):
-                _lib.failure_configs(0)
+        if bad:  # the failure report straight from the HBM tables, as sets
+            _check_configs_vs_oracle(h, f"wide w={w}")
     h = synth.gen_register(2000, 16, 0.002, 0x5EED4000 + 13, n_crashed=13)
     assert _live_width(h, 0) == 27
     g = _lib.check(1, 0, h)
     assert _lib.check_stats()["wide_histories"] == 1
     assert int(g["valid"][0]) == 1 and int(g["explored"][0]) > 0
+
+
+def _check_configs_vs_oracle(h, what, k=1 << 12):
+    """lc_failure_configs of history 0 of the last check against the oracle's pre-failure frontier:
+    the configs as a set, each config's :last-op, the newest, the pending ops."""
+    e = oracle.check_one("cas-register", h, with_configs=True)
+    assert e["valid"] == 0, what
+    cfgs, pending, lasts, newest = _lib.failure_configs(0, k, with_last=True)
+    assert sorted(pending) == sorted(e["pending_inv_idx"]), what
+    assert set(cfgs) == e["fail_configs"] and len(cfgs) == len(e["fail_configs"]), what
+    for c, last in zip(cfgs, lasts):
+        assert last == e["fail_last_op"][c], (what, c, last, e["fail_last_op"][c])
+    assert newest == max(e["fail_last_op"].values()), what
+    return sum(1 for x in lasts if x != e["prev_ok_idx"])
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_gpu_wide_failure_configs_match_oracle(pipe, monkeypatch):
+    """failure reports from the HBM tables (wide.hip: a re-run stopped before
+    the failing RETURN, the frontier dumped from the table, each config's :last-op walked back
+    through the final tables, re-running to earlier stops for long walks). Every history forced
+    onto the tables (LC_WIDE_MINW=1), both table layouts (pipelined: ranked; one step at a
+    time: natural), against the oracle: configs as sets, per-config :last-op, the newest, and
+    the grid kernel's report (LC_WIDE_CONFIGS=0) on the same history."""
+    monkeypatch.setenv("LC_WIDE_MINW", "1")
+    monkeypatch.setenv("LC_WIDE_PIPE", pipe)
+    found = carried = 0
+    for t in range(30):
+        h = synth.gen_register(80, 4, 0.1, 9000 + t, invalid=True, n_crashed=t % 3)
+        g = _lib.check(1, 0, h)
+        assert _lib.check_stats()["wide_histories"] == 1
+        e = oracle.check_one("cas-register", h)
+        assert int(g["valid"][0]) == e["valid"]
+        if e["valid"] != 0:
+            continue
+        carried += _check_configs_vs_oracle(h, f"t={t}")
+        found += 1
+        if t % 5 == 0:  # the same report through the grid kernel's tagged re-run
+            a = _lib.failure_configs(0, 1 << 12, with_last=True)
+            monkeypatch.setenv("LC_WIDE_CONFIGS", "0")
+            b = _lib.failure_configs(0, 1 << 12, with_last=True)
+            monkeypatch.delenv("LC_WIDE_CONFIGS")
+            assert a == b, t
+    assert found > 5 and carried > 0
 
 
 def test_gpu_wide_tables_past_31_slots():
@@ -1189,6 +1232,8 @@ def test_gpu_wide_tables_past_31_slots():
         e = oracle.check_one("cas-register", h)
         _cmp(g, e, 0, f"wide w={w}")
         assert int(g["explored"][0]) == oracle.check_one("cas-register", base)["explored"]
+        if bad and e["valid"] == 0:
+            _check_configs_vs_oracle(h, f"wide w={w}")
 
 
 def test_gpu_wide_watchdog_abort_is_unknown(monkeypatch):
