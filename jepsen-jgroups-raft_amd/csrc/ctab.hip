@@ -28,6 +28,8 @@
 #include "ctab.hpp"
 #include "dense.hpp"
 #include "search.hpp"
+#include "dense_ops.hpp"
+#include "device_common.hpp"
 
 namespace lc {
 namespace {
@@ -45,6 +47,8 @@ struct __attribute__((aligned(16))) CStep {
   uint32_t live, fresh, anyx;
   int32_t base;              // sum of the deltas of the ops returned before this step
   int32_t j, jp, H, start;   // returning slot, previous step's, layers - 1, first super-layer
+  int32_t pstart, hpl, Hl, tb;  // tile teams: the previous step's start and local layers - 1, this
+                                // step's local layers - 1 and live team bits (ctab_team_kernel)
   uint64_t keep_lo;          // positions without a fresh low slot
   int32_t req[32];           // per slot: requirement relative to init (CQ_UNC / CQ_NEVER)
   int32_t cq[32];            // per slot: EQ index base (k < 6: req - base - lo_min; k >= 6: + d_k)
@@ -183,8 +187,11 @@ __device__ __forceinline__ uint64_t ct_x(const uint64_t* B, uint32_t w, uint32_t
 // One step's closure of word w (its frontier X): the hi pulls and the in-word closure. Returns R.
 // pf (builds with LC_CT_WORDPROF and LC_DEBUG, else null): cycles to the hi sums, the pulls, the
 // gates, the closure; closure sweeps. (Compiled out by default: the checks alone cost C2c 3 %.)
+// wg: the word's hi bits over the whole table (a tile team's tile holds the words w | rank << lb),
+// which set its delta sum; R0: pulls already made from other tiles (gated).
 __device__ __forceinline__ uint64_t ct_word(const uint64_t* Bt, uint32_t w, const CStep* st, uint32_t live, int j,
-                                            uint64_t X, unsigned long long* pf = nullptr) {
+                                            uint64_t X, uint32_t wg, uint64_t R0,
+                                            unsigned long long* pf = nullptr) {
 #ifdef LC_CT_WORDPROF
   unsigned long long tp = pf ? __builtin_amdgcn_s_memtime() : 0;
   auto pmark = [&](int k) {
@@ -198,12 +205,13 @@ __device__ __forceinline__ uint64_t ct_word(const uint64_t* Bt, uint32_t w, cons
 #else
   auto pmark = [](int) {};
 #endif
-  const int s_hi = (int)st->sh[0][w & 127u] + (int)st->sh[1][(w >> 7) & 127u];
+  const int s_hi = (int)st->sh[0][wg & 127u] + (int)st->sh[1][(wg >> 7) & 127u];
   pmark(0);
   const bool jhi = j >= CTAB_LO;
-  const uint32_t jh = jhi ? 1u << (j - CTAB_LO) : 0u;
+  // (a tile team's j above the tile's local slots gives jh 0 here: that tile pulls it remotely)
+  const uint32_t jh = jhi && j - CTAB_LO < 32 ? 1u << (j - CTAB_LO) : 0u;
   uint32_t m = (w & jh) ? jh : w;
-  uint64_t R = 0;
+  uint64_t R = R0;
   while (m) {  // the word's set hi bits, two at a time (their loads issued together; r4b A/B: a batch
                // of four with every EQ lookup issued at once was 3 % slower on C2c)
     int b[2];
@@ -453,9 +461,9 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
         // (r4k: wave-uniform control flow in the word, every lane through every pull round and
         // closure sweep with masked loads, was 8 % slower on C2c4: the divergent form is kept)
         #ifdef LC_CT_WORDPROF
-        const uint64_t R = ct_word(Bt, w, st, live, j, X, prof ? pw : nullptr);
+        const uint64_t R = ct_word(Bt, w, st, live, j, X, w, 0ull, prof ? pw : nullptr);
 #else
-        const uint64_t R = ct_word(Bt, w, st, live, j, X);
+        const uint64_t R = ct_word(Bt, w, st, live, j, X, w, 0ull);
 #endif
         Bt[w] = X | R;
         expl += (uint32_t)__popcll(R);
@@ -543,6 +551,353 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_kernel(CtabParams p) {
   if (lane == 0 && st_steps) atomicAdd(&p.stats[1], st_steps);
 }
 
+// ---- counter tile teams (ctab.hpp CtabTeamParams) ----------------------------
+// One history per team of G = 2^T workgroups: tile r holds the masks whose team slots (lb..lb+T-1)
+// spell r, its table over the lb local slots in LDS (2^(lb-6) words, double-buffered when two
+// fit). Every tile walks the step stream itself and runs the LDS kernel's pipelined schedule over
+// its local layers, shifted by its live team slots (tile r's layer q of step t at super-layer
+// start_t + q + |r|), so a step spans Hl + tb + 1 super-layers. Hand-offs (the schedule of
+// dense.hip's pipelined tile teams with global layers, r2):
+//  * a wide step's words (some team slot live) are stored sc1 into the tile's mirror slot for the
+//    step, in layer order (cum[Hl][q] + the word's index in its layer); after its super-layer each
+//    tile drains its stores and stores its token = super-layers finished;
+//  * a pull over team slot b reads tile r \ b's mirror word, finished one super-layer earlier
+//    (token >= s); a tile holding the returning team slot j takes only T_j of tile r \ j;
+//  * after a team-slot return jp the X of tile r is tile r | jp's word of the previous step,
+//    finished at pstart + q + |r| + 1 (token >= pstart + q + |r| + 2);
+//  * every CTT_CW super-layers a tile waits until no tile is more than CTT_CW behind, so a
+//    mirror slot (reused CT_MRING steps later) is never rewritten while a reader lags.
+// Failures: a tile that read a nonzero X in step t sets the team's bit t; after the last step
+// (and its return, checked tile by tile) the first missing bit t names step t - 1. An empty
+// frontier stays empty, so the explored count of the steps after a failure is 0.
+constexpr int CTT_RING = 24;
+constexpr int CTT_CAPW = 1 << 13;  // LDS table words of a tile (64 KiB: two tables of <= 2^12 words)
+constexpr int CTT_CW = 8;          // credit window (super-layers)
+
+__device__ __forceinline__ bool ct_poll(const CtabTeamParams& tp, const unsigned long long* f,
+                                        unsigned long long need, uint64_t t0, long& spins) {
+  if (ld_agent(f) >= need) return true;
+  __builtin_amdgcn_s_sleep(1);
+  if ((++spins & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > tp.watchdog || ld_agent(tp.abort))) {
+    st_agent(tp.abort, 1);
+    return true;  // gives up: the caller sees the abort word
+  }
+  return false;
+}
+
+// all G workgroups of a team: every wave's stores drained, one arrival each, the last one bumps
+// the generation (ctl[32]) the others poll; false when a watchdog fired
+__device__ __forceinline__ bool ct_team_bar(const CtabTeamParams& tp, unsigned* ctl, int G, int* sAbort) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned g = ld_agent(&ctl[32]);
+    if (__hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1) {
+      st_agent(&ctl[0], 0u);
+      __hip_atomic_store(&ctl[32], g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      long spins = 0;
+      while (ld_agent(&ctl[32]) == g) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > tp.watchdog || ld_agent(tp.abort))) {
+          st_agent(tp.abort, 1);
+          break;
+        }
+      }
+    }
+    *sAbort = ld_agent(tp.abort);
+  }
+  __syncthreads();
+  return *sAbort == 0;
+}
+
+__global__ void __launch_bounds__(CT_TEAM) ctab_team_kernel(CtabTeamParams tp) {
+  const CtabParams& p = tp.c;
+  __shared__ uint64_t sTab[CTT_CAPW];
+  __shared__ CStep sRing[CTT_RING];
+  __shared__ uint32_t sBinom[CT_BINOM * CT_BINOM];
+  __shared__ uint32_t sCum[CT_BINOM * CT_BINOM];  // cum[H][q] = sum_{p < q} C(H, p): layer q's first index
+  __shared__ uint32_t sWOff[CT_BINOM + 2];
+  __shared__ int sAbort, sFail;
+  __shared__ unsigned long long sExpl;
+  const int tt = threadIdx.x, lane = tt & 63;
+  const bool decoder = tt < 64;
+  const int team = tp.wg_team[blockIdx.x];
+  const int base = tp.team_base[team], rank = (int)blockIdx.x - base, T = tp.team_bits[team], G = 1 << T;
+  const int h = tp.team_hist[team];
+  init_binom(sBinom, tt, CT_TEAM);
+  if (tt <= DENSE_WORD_BITS + 1) {  // offsets of the global list's popcount layers
+    uint32_t o = 0;
+    for (int q = 0; q < tt; ++q) {
+      uint64_t v = 1;
+      for (int i = 1; i <= q; ++i) v = v * (uint64_t)(DENSE_WORD_BITS - q + i) / (uint64_t)i;
+      o += (uint32_t)v;
+    }
+    sWOff[tt] = o;
+  }
+  if (tt == 0) sAbort = 0, sExpl = 0, sFail = INT32_MAX;
+  __syncthreads();
+  if (tt < CT_BINOM * CT_BINOM) {
+    const int n = tt / CT_BINOM, q = tt % CT_BINOM;
+    uint32_t c = 0;
+    for (int r = 0; r < q; ++r) c += sBinom[n * CT_BINOM + r];
+    sCum[tt] = c;
+  }
+  const int lmax = p.lmax[h], ns = p.nsteps[h];
+  const int lb = lmax - T, Hm = lb > CTAB_LO ? lb - CTAB_LO : 0;
+  const uint32_t lmask = (1u << lb) - 1u;
+  const int NW = 1 << Hm;
+  const bool dbl = (p.pipe & CT_PIPE_DBL) && 2 * NW <= CTT_CAPW;
+  uint64_t* const B = sTab;
+  uint64_t* const B2 = dbl ? sTab + NW : sTab;
+  auto tab = [&](int t) { return (t & 1) ? B2 : B; };
+  const int ntab = dbl ? 2 * NW : NW;
+  for (int i = tt; i < ntab; i += CT_TEAM) sTab[i] = 0;
+  const uint32_t* words = p.words;
+  const uint32_t* wofs = sWOff;
+  uint32_t* const lw = reinterpret_cast<uint32_t*>(sTab + ntab);
+  uint32_t* const lo = lw + NW;
+  const bool lds_list = Hm > 0 && ntab + NW / 2 + 16 <= CTT_CAPW;
+  __syncthreads();
+  if (lds_list) {
+    if (tt <= Hm + 1) lo[tt] = sCum[Hm * CT_BINOM + tt];
+    for (int q = 0; q <= Hm; ++q) {
+      const uint32_t nq = sBinom[Hm * CT_BINOM + q], og = sWOff[q], ol = sCum[Hm * CT_BINOM + q];
+      for (uint32_t r = (uint32_t)tt; r < nq; r += (uint32_t)CT_TEAM) lw[ol + r] = p.words[og + r];
+    }
+    words = lw, wofs = lo;
+  }
+  unsigned long long* const flags = tp.flags + base;
+  uint32_t* const anyv = tp.anyv + tp.team_any_off[team];
+  auto mirror = [&](int r, int t) {
+    return tp.mirror + (((size_t)(base + r) * CT_MRING + (size_t)(t % CT_MRING)) << tp.mshift);
+  };
+  if (p.stamps && rank == 0 && tt == 0) p.stamps[2 * h] = __builtin_amdgcn_s_memrealtime();
+  __syncthreads();
+  if (rank == 0 && tt == 0) B2[0] = 1;  // the initial config (step 0 reads tab(-1))
+  StreamWin sw;
+  int64_t pos = p.sbeg[h];
+  // decode a step, then its tile-team fields (local layers - 1, live team slots, the previous
+  // step's local layers - 1)
+  auto decode = [&](int t) {
+    CStep* dst = &sRing[t % CTT_RING];
+    const CStep* prev = t > 0 ? &sRing[(t - 1) % CTT_RING] : nullptr;
+    ct_decode(p, sw, pos, lane, dst, prev);
+    if (lane == 0) {
+      const uint32_t live = dst->live;
+      const int L = live ? 32 - __clz((int)live) : 0;
+      const int Ll = L < lb ? L : lb;
+      dst->Hl = Ll > CTAB_LO ? Ll - CTAB_LO : 0;
+      dst->tb = __popc(live >> lb);
+      dst->hpl = prev ? prev->Hl : 0;
+      dst->pstart = 0;
+    }
+  };
+  if (ns > 0 && decoder) {
+    decode(0);
+    if (lane == 0) sRing[0].start = 0;
+  }
+  __syncthreads();
+  unsigned long long expl = 0, st_fout = 0;
+  int t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0, last_start = 0;
+  int s = 0;
+  for (; t_ret < ns; ++s) {
+    if (s >= CTT_CW && (s % CTT_CW) == 0) {  // credit: nobody more than CTT_CW super-layers behind
+      if (decoder) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        long spins = 0;
+        while (!__all(lane >= G || ct_poll(tp, &flags[lane < G ? lane : 0], (unsigned long long)(s - CTT_CW), t0, spins)))
+          ;
+        if (lane == 0) sAbort = ld_agent(tp.abort);
+      }
+      __syncthreads();
+      if (sAbort) break;
+    }
+    // ---- ring view: lane i = step t_ret + i
+    const int tl = t_ret + lane;
+    const bool dec_l = lane < CTT_RING && tl < t_dec;
+    uint4 h0 = {0u, 0u, 0u, 0u};
+    int4 h1 = {0, 0, 0, 1 << 30}, h2 = {0, 0, 0, 0};
+    if (dec_l) {
+      const CStep* st = &sRing[tl % CTT_RING];
+      h0 = *reinterpret_cast<const uint4*>(&st->live);    // live, fresh, anyx, base
+      h1 = *reinterpret_cast<const int4*>(&st->j);        // j, jp, H, start
+      h2 = *reinterpret_cast<const int4*>(&st->pstart);   // pstart, hpl, Hl, tb
+    }
+    const bool run_l = dec_l && tl < t_run;
+    const bool fin_l = run_l && h1.w + h2.z + h2.w < s;
+    const uint64_t fin = __ballot(fin_l);
+    const int lead = (int)__builtin_ctzll(~fin);
+    if (decoder && lane < lead && tl > 0 && h0.z)  // retired: this tile read a config in step tl
+      __hip_atomic_fetch_or(&anyv[tl >> 5], 1u << (tl & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int t_ret_old = t_ret;
+    t_ret += lead;
+    if (t_ret >= ns) break;
+    // ---- this tile's segments: running steps whose live team slots cover the tile
+    const uint32_t lteam_l = h0.x >> lb;
+    const int dr_l = __popc((uint32_t)rank & lteam_l);
+    const int q_l = s - h1.w - dr_l;
+    const bool seg_l = run_l && ((uint32_t)rank & ~lteam_l) == 0 && q_l >= 0 && q_l <= h2.z;
+    uint32_t nq_l = 0, o_l = 0, mo_l = 0, mp_l = 0, pm_l = 0;
+    int xs_l = -1;
+    if (seg_l) {
+      nq_l = sBinom[h2.z * CT_BINOM + q_l], o_l = wofs[q_l], mo_l = sCum[h2.z * CT_BINOM + q_l];
+      mp_l = sCum[h2.y * CT_BINOM + min(q_l, h2.y)];
+      const int jt = h1.x >= lb ? h1.x - lb : -1;
+      const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
+      pm_l = lteam_l == 0 ? 0u : tile_j ? (1u << jt) : ((uint32_t)rank & lteam_l);
+      if (h1.y >= lb && !((uint32_t)rank & (h0.y >> lb))) xs_l = rank | (1 << (h1.y - lb));
+    }
+    if (__any(pm_l != 0 || xs_l >= 0)) {  // wait for the tiles this super-layer reads
+      if (decoder) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        long spins = 0;
+        for (;;) {
+          bool ok = true;
+          for (uint32_t m = pm_l; m && ok; m &= m - 1)
+            ok = ct_poll(tp, &flags[rank ^ (1 << __builtin_ctz(m))], (unsigned long long)s, t0, spins);
+          if (ok && xs_l >= 0)
+            ok = ct_poll(tp, &flags[xs_l], (unsigned long long)(h2.x + q_l + dr_l + 2), t0, spins);
+          if (__all(ok)) break;
+        }
+        if (lane == 0) sAbort = ld_agent(tp.abort);
+      }
+      __syncthreads();
+      if (sAbort) break;
+    }
+    const uint64_t segm = __ballot(seg_l);
+    const bool wide_any = __ballot(seg_l && lteam_l != 0) != 0;
+    uint32_t total = 0;
+    for (uint64_t m = segm; m; m &= m - 1) total += (rdl(nq_l, (int)__builtin_ctzll(m)) + 63u) & ~63u;
+    for (uint32_t f0 = (uint32_t)(tt & ~63); f0 < total; f0 += (uint32_t)CT_TEAM) {
+      int i = 0;
+      uint32_t e = 0, acc = 0;
+      for (uint64_t m = segm; m; m &= m - 1) {
+        const int k = (int)__builtin_ctzll(m);
+        if (f0 >= acc) i = k, e = acc;
+        acc += (rdl(nq_l, k) + 63u) & ~63u;
+      }
+      const uint32_t nq = rdl(nq_l, i), r = f0 - e + (uint32_t)lane;
+      const uint32_t mo = rdl(mo_l, i), mp = rdl(mp_l, i), pmask = rdl(pm_l, i), o = rdl(o_l, i);
+      const uint32_t live = rdl(h0.x, i), fresh = rdl(h0.y, i);
+      const int j = rdl(h1.x, i), jp = rdl(h1.y, i), xs = rdl(xs_l, i);
+      const int t = t_ret_old + i;
+      if (r >= nq) continue;
+      const uint32_t w = words[o + r];
+      const uint32_t live_loc = live & lmask, lteam = live >> lb;
+      if (w & ~(live_loc >> CTAB_LO)) continue;
+      const bool wide = lteam != 0;
+      const int jt = j >= lb ? j - lb : -1;
+      const bool tile_j = jt >= 0 && ((rank >> jt) & 1);
+      const bool jloc_hi = j >= CTAB_LO && j < lb;
+      const bool tile_fresh = ((uint32_t)rank & (fresh >> lb)) != 0;
+      const uint32_t fresh_hi = (fresh & lmask) >> CTAB_LO;
+      CStep* st = &sRing[t % CTT_RING];
+      uint64_t* const Bt = tab(t);
+      const uint32_t wg = w | ((uint32_t)rank << Hm);  // the word's hi bits over the whole table
+      const uint64_t keep_lo = st->keep_lo;
+      const bool fx = !tile_fresh && !(w & fresh_hi);
+      // HBM loads first (X from tile xs, the pulls from the tiles one team slot below), used after
+      uint64_t X = 0, pv[CTAB_TEAM_MAXB];
+      if (fx && xs >= 0) X = HbmTab::ld(mirror(xs, t - 1) + mp + r);
+      const bool pl = tile_j || !(jloc_hi && ((w >> (j - CTAB_LO)) & 1u));
+#pragma unroll
+      for (int b = 0; b < CTAB_TEAM_MAXB; ++b)
+        pv[b] = (pl && ((pmask >> b) & 1u)) ? HbmTab::ld(mirror(rank ^ (1 << b), t) + mo + r) : 0ull;
+      if (xs >= 0) X &= keep_lo;
+      else if (fx) X = ct_x(tab(t - 1), w, 0u, jp, keep_lo);
+      const int s_hi = (int)st->sh[0][wg & 127u] + (int)st->sh[1][(wg >> 7) & 127u];
+      uint64_t R0 = 0;
+#pragma unroll
+      for (int b = 0; b < CTAB_TEAM_MAXB; ++b)
+        if ((pmask >> b) & 1u) R0 |= pv[b] & gate(st, st->cq[CTAB_LO + Hm + b], s_hi);
+      const uint64_t R = tile_j ? R0 : ct_word(Bt, w, st, live, j, X, wg, R0);
+      const uint64_t nv = X | R;
+      Bt[w] = nv;
+      if (wide) HbmTab::st(mirror(rank, t) + mo + r, nv);
+      expl += (uint32_t)__popcll(R);
+      if (t > 0) st_fout += (uint32_t)__popcll(X);
+      if (X) st->anyx = 1;
+    }
+    // ---- decode ahead into a slot nobody read in this super-layer
+    const int t_dec_old = t_dec;
+    if (t_dec < ns && t_dec - t_ret_old < CTT_RING) {
+      if (decoder) decode(t_dec);
+      ++t_dec;
+    }
+    // ---- start the next decoded step at s + 1: two super-layers after its predecessor (one after
+    // an in-word return on double-buffered tables, or the predecessor's whole span if shorter),
+    // at once if the predecessor retired
+    if (t_run < t_dec_old) {
+      const int lp = t_run - 1 - t_ret_old;
+      bool ok = lp < 0 || lp < lead;
+      if (!ok) {
+        const int gap = (dbl && rdl(h1.x, lp) < CTAB_LO) ? 1 : 2;
+        ok = s + 1 - rdl(h1.w, lp) >= min(gap, rdl(h2.z, lp) + rdl(h2.w, lp) + 1);
+      }
+      if (ok) {
+        if (tt == 0) sRing[t_run % CTT_RING].start = s + 1, sRing[t_run % CTT_RING].pstart = last_start;
+        last_start = s + 1;
+        ++t_run;
+      }
+    }
+    if (wide_any) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+    if (tt == 0) st_agent(&flags[rank], (unsigned long long)(s + 1));
+  }
+  unsigned* const ctl = tp.ctl + 64 * team;
+  // the last step's return, tile by tile, once every tile has finished
+  if (ct_team_bar(tp, ctl, G, &sAbort) && ns > 0) {
+    const CStep* st = &sRing[(ns - 1) % CTT_RING];
+    const int jl = rfl(st->j);
+    const uint32_t live = (uint32_t)rfl((int)st->live);
+    const uint32_t lteam = live >> lb;
+    const int jt = jl >= lb ? jl - lb : -1;
+    // a team-slot j: the post-return frontier of tile r \ j is tile r's own words (its masks hold j)
+    const bool mine = jt >= 0 ? (((uint32_t)rank & ~lteam) == 0 && ((rank >> jt) & 1))
+                              : ((uint32_t)rank & ~lteam) == 0;
+    uint64_t nzx = 0;
+    if (mine) {
+      const uint32_t lhi = ((live & ~(jt >= 0 ? 0u : 1u << jl)) & lmask) >> CTAB_LO;
+      const int nwt = 1 << Hm;
+      for (int w = tt; w < nwt; w += CT_TEAM) {
+        if ((uint32_t)w & ~lhi) continue;
+        const uint64_t X = jt >= 0 ? tab(ns - 1)[w] : ct_x(tab(ns - 1), (uint32_t)w, 0u, jl, ~0ull);
+        st_fout += (uint32_t)__popcll(X);
+        nzx |= X;
+      }
+    }
+    if (__syncthreads_or(nzx != 0) && tt == 0)
+      __hip_atomic_fetch_or(&anyv[ns >> 5], 1u << (ns & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
+  if (lane == 0 && expl) atomicAdd(&sExpl, expl);
+  __syncthreads();
+  if (tt == 0 && sExpl) atomicAdd(&p.explored[h], sExpl);
+  const bool done = ct_team_bar(tp, ctl, G, &sAbort);
+  if (done && rank == 0) {  // the first step whose frontier was empty everywhere
+    for (int wd = tt; wd <= (ns >> 5); wd += CT_TEAM) {
+      uint32_t v = ld_agent(&anyv[wd]);
+      if (wd == 0) v |= 1u;  // (step 0 reads the initial config)
+      const int top = ns - 32 * wd;  // bits 0..min(31, top) are steps
+      const uint32_t need = top >= 31 ? ~0u : ((1u << (top + 1)) - 1u);
+      const uint32_t miss = ~v & need;
+      if (miss) atomicMin(&sFail, 32 * wd + __builtin_ctz(miss));
+    }
+    __syncthreads();
+    if (tt == 0) {
+      const int fail_t = sFail == INT32_MAX ? -1 : sFail - 1;
+      p.fail_step[h] = fail_t;
+      p.status[h] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      if (p.stamps) p.stamps[2 * h + 1] = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(&p.stats[1], (unsigned long long)(fail_t >= 0 ? fail_t + 1 : ns));
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) st_fout += __shfl_down(st_fout, off, 64);
+  if (lane == 0 && st_fout) atomicAdd(&p.stats[0], st_fout);
+}
+
 }  // namespace
 
 int ctab_grid_size() {
@@ -551,6 +906,20 @@ int ctab_grid_size() {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ctab_kernel, CT_TEAM, 0) != hipSuccess) return 0;
   return ncu * per;
+}
+
+int ctab_team_max_wgs() {
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ctab_team_kernel, CT_TEAM, 0) != hipSuccess) return 0;
+  return ncu * per;
+}
+
+hipError_t launch_ctab_team(const CtabTeamParams& p, int grid, hipStream_t stream) {
+  CtabTeamParams q = p;
+  void* args[] = {&q};
+  return hipLaunchCooperativeKernel((const void*)ctab_team_kernel, dim3(grid), dim3(CT_TEAM), args, 0, stream);
 }
 
 hipError_t launch_ctab(const CtabParams& p, int grid, hipStream_t stream) {

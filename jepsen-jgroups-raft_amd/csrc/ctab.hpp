@@ -61,4 +61,34 @@ struct CtabParams {
 hipError_t launch_ctab(const CtabParams& p, int grid, hipStream_t stream);
 int ctab_grid_size();
 
+// Counter tile teams: ONE counter history's table split
+// over 2^T workgroups by its top T slots (the team slots lb..lb+T-1, lb = lmax - T). Tile r holds
+// the masks whose team slots spell r, over its lb local slots, in LDS; a pull over a team slot
+// reads tile r \ b's word from that tile's mirror in HBM (sc1 stores, drained, then a token =
+// super-layers finished), and so does the X of a step after a team-slot return (tile r | jp).
+// The super-layer schedule is the LDS kernel's, skewed per tile: tile r runs its local layer q
+// of step t at super-layer start_t + q + |r| (|r| = its live team slots), so whatever it pulls
+// from another tile was finished one super-layer earlier. One cooperative launch: every team's
+// workgroups are resident together.
+constexpr int CT_MRING = 64;  // mirror slots per tile (steps)
+constexpr int CTAB_TEAM_MAXB = 4;  // team slots (16 tiles)
+struct CtabTeamParams {
+  CtabParams c;                  // sbeg, nsteps, lmax, words, stream, status, fail_step, explored, stats, stamps
+  int32_t n_teams;
+  const int32_t* wg_team;        // [grid] the team of each workgroup
+  const int32_t* team_base;      // [n_teams] its first workgroup
+  const int8_t* team_bits;       // [n_teams] T (2^T tiles)
+  const int32_t* team_hist;      // [n_teams] plan-local history id
+  const int32_t* team_any_off;   // [n_teams] first word of the team's per-step survivor bits
+  unsigned long long* flags;     // [grid] tokens: super-layers the tile has finished (zeroed)
+  uint64_t* mirror;              // [grid][CT_MRING][2^mshift] published words
+  int32_t mshift;
+  uint32_t* anyv;                // per team, bit t: a tile read a nonzero frontier in step t (zeroed)
+  unsigned* ctl;                 // per team 64 words: barrier arrivals [0], generation [32] (zeroed)
+  int32_t* abort;                // a watchdog fired (zeroed)
+  uint64_t watchdog;             // s_memrealtime ticks a wait may last before *abort
+};
+hipError_t launch_ctab_team(const CtabTeamParams& p, int grid, hipStream_t stream);
+int ctab_team_max_wgs();  // workgroups one cooperative team launch may hold
+
 }  // namespace lc

@@ -168,6 +168,11 @@ struct lc_plan {
   int dgrid_c = 0;
   int ctab_maxw = CTAB_LMAX;  // LC_CTAB_MAXW (0: counters take the grid kernel, tests)
   int ctab_pipe = 3;          // LC_CTAB_PIPE: bit 0 double-buffered tables, bit 1 chunks from an LDS counter
+  // counter tile teams (ctab_team_kernel): LC_CTAB_TEAM=0 keeps every counter on one
+  // workgroup; histories of live width >= LC_CTAB_TEAM_MINW get 2^T tiles, T = LC_CTAB_TEAM_T or,
+  // by default, width - 17 clamped to 1..3 (tiles of <= 17 local slots: 2^11 words, double-buffered)
+  int ctab_team = 1, ctab_team_minw = 16, ctab_team_t = 0;
+  std::vector<int8_t> ctab_T;  // per history: team slots (0: one workgroup)
   DevArray d_cstats;
   DevArray d_dpack, d_dwords, d_dqueue, d_dstatus, d_dfail, d_dexpl;
   DevArray d_dres;  // run_dense's results in one block: explored | status | fail | stats | abort | stamps
@@ -176,6 +181,7 @@ struct lc_plan {
   std::vector<char> wide_ok;
   std::vector<std::vector<uint32_t>> wide_streams;  // per history (built by dense_sink)
   DevArray d_wtab, d_wstream, d_wmeta, d_wres, d_wbar;
+  DevArray d_ctmeta, d_ctmirror, d_ctctl, d_ctord;  // counter tile teams
   int wide_maxw = WIDE_LMAX, wide_minw = 0;  // LC_WIDE_MAXW (0: off) / LC_WIDE_MINW (tests)
   int wide_grid = 0;  // LC_WIDE_GRID: at most this many workgroups for the HBM tables (0: all resident)
   int wide_watchdog_ms = 20000;  // LC_WIDE_WATCHDOG_MS: a grid barrier's longest wait
@@ -382,6 +388,9 @@ struct lc_plan {
     }
     if ((e = getenv("LC_CTAB_MAXW"))) ctab_maxw = std::max(0, std::min(atoi(e), CTAB_LMAX));
     if ((e = getenv("LC_CTAB_PIPE"))) ctab_pipe = atoi(e);
+    if ((e = getenv("LC_CTAB_TEAM"))) ctab_team = atoi(e);
+    if ((e = getenv("LC_CTAB_TEAM_MINW"))) ctab_team_minw = atoi(e);
+    if ((e = getenv("LC_CTAB_TEAM_T"))) ctab_team_t = std::max(0, std::min(atoi(e), CTAB_TEAM_MAXB));
     if ((e = getenv("LC_TILE_LBITS")) && atoi(e) > 0) tile_lbits = std::max(12, std::min(atoi(e), DENSE_LMAX));
     if ((e = getenv("LC_PIPE"))) dense_pipe = atoi(e), pipe_env = true;
     if ((e = getenv("LC_TEAM_PLAN"))) plan_off = atoi(e) == 0;
@@ -419,6 +428,7 @@ struct lc_plan {
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
     ctab_maxw = CTAB_LMAX, ctab_pipe = 3, wide_watchdog_ms = 20000, wide_force_abort = false;
+    ctab_team = 1, ctab_team_minw = 16, ctab_team_t = 0;
     wide_stall_hist = wide_stall_wg = -1;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
@@ -554,6 +564,7 @@ struct lc_plan {
     if (!dense_on) return 0;
     dense_ok.assign(n, 0);
     wide_ok.assign(n, 0);
+    ctab_T.assign(n, 0);
     if ((int)wide_streams.size() < n) wide_streams.resize(n);
     dense_cost.assign(n, 0.0);
     dense_nw.assign(n, 0);
@@ -703,6 +714,42 @@ struct lc_plan {
     dense_ok[h] = 1;
     nst[h] = (int32_t)v.n_steps;
     lm[h] = (int8_t)std::max(1, v.live_max);
+    // a tile team (ctab_team_kernel) for a wide history: its team slots are the top T positions
+    // of the table. Slot labels are arbitrary (a mask is a set), so the T hi slots live in the
+    // most steps take those positions (every step then spreads over the tiles; crashed ops, live
+    // for good and never returning, are the best team slots); the other hi slots keep their order.
+    const int Lh = v.live_max;
+    int T = 0;
+    if (ctab_team && Lh >= ctab_team_minw)
+      T = ctab_team_t > 0 ? ctab_team_t : std::max(1, std::min(3, Lh - 17));
+    if (Lh - T < CTAB_LO + 1) T = 0;
+    ctab_T[h] = (int8_t)T;
+    uint32_t pi[32];
+    for (int k = 0; k < 32; ++k) pi[k] = (uint32_t)k;
+    if (T > 0) {
+      int64_t cnt[32] = {0};
+      uint32_t lv = 0;
+      int64_t q = 0;
+      for (int64_t t = 0; t < v.n_steps; ++t) {
+        if (t > 0) lv &= ~(1u << v.step_slot[t - 1]);
+        for (int64_t k = q; k < q + v.step_ninv[t]; ++k) lv |= 1u << v.inv_slot[k];
+        q += v.step_ninv[t];
+        for (uint32_t m = lv; m; m &= m - 1) ++cnt[__builtin_ctz(m)];
+      }
+      std::vector<int> hi;
+      for (int k = CTAB_LO; k < Lh; ++k) hi.push_back(k);
+      std::stable_sort(hi.begin(), hi.end(), [&](int a, int b) { return cnt[a] > cnt[b]; });
+      std::vector<char> team(32, 0);
+      for (int i = 0; i < T; ++i) team[hi[i]] = 1, pi[hi[i]] = (uint32_t)(Lh - T + i);
+      uint32_t nxt = CTAB_LO;
+      for (int k = CTAB_LO; k < Lh; ++k)
+        if (!team[k]) pi[k] = nxt++;
+    }
+    auto relabel = [&](uint32_t m) {
+      uint32_t r = 0;
+      for (; m; m &= m - 1) r |= 1u << pi[__builtin_ctz(m)];
+      return r;
+    };
     uint32_t* const out0 = (uint32_t*)hpack + ((const int64_t*)(hpack + o_sbeg))[h];
     uint32_t* out = out0;
     const int64_t init = enc.init_value;
@@ -713,7 +760,7 @@ struct lc_plan {
       if (t > 0) live &= ~(1u << v.step_slot[t - 1]);
       const int64_t q1 = q + v.step_ninv[t];
       for (int64_t k = q; k < q1; ++k) live |= 1u << v.inv_slot[k];
-      *out++ = live | ((uint32_t)v.step_slot[t] << DENSE_J_SHIFT);
+      *out++ = relabel(live) | (pi[v.step_slot[t]] << DENSE_J_SHIFT);
       for (int64_t k = q; k < q1; ++k) {
         const uint8_t kind = v.inv_kind[k];
         const int64_t a = v.inv_a[k], delta = (kind & C_SUB) ? -v.inv_b[k] : v.inv_b[k];
@@ -731,7 +778,7 @@ struct lc_plan {
           if (req >= CTAB_REQ_BIAS || req < -CTAB_REQ_BIAS) never = true;  // no config reaches it
           if (never) fl = CT_NEVER, req = 0;
         }
-        *out++ = (uint32_t)v.inv_slot[k] | (fl << 8) | ((uint32_t)(uint8_t)(int8_t)delta << 16) | DENSE_OPW;
+        *out++ = pi[v.inv_slot[k]] | (fl << 8) | ((uint32_t)(uint8_t)(int8_t)delta << 16) | DENSE_OPW;
         *out++ = ((uint32_t)(req + CTAB_REQ_BIAS) & 0x3fffffffu) | DENSE_OPW;
       }
       const int L = live ? 32 - __builtin_clz(live) : 0;
@@ -1727,9 +1774,102 @@ struct lc_plan {
       HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, 16 * 12 * 8, stream));
       p.prof = d_dlhist.as<unsigned long long>();
     }
-    const int grid = std::min(nc, dgrid_c);
+    // tile teams first (one cooperative launch, the widest histories while their workgroups fit),
+    // then every other counter history one per workgroup; both write the same result arrays
+    std::vector<int32_t> t_hist, t_base, t_anyoff, wg_team;
+    std::vector<int8_t> t_bits;
+    std::vector<int32_t> singles;
+    {
+      const int cap = std::min(ctab_team_max_wgs(), 256);
+      int used = 0, anyw = 0;
+      std::vector<int> cand;
+      for (int h : dense_c)
+        if (ctab_T[h] > 0) cand.push_back(h);
+      std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return dense_cost[a] > dense_cost[b]; });
+      std::vector<char> in_team(n, 0);
+      for (int h : cand) {
+        const int g = 1 << ctab_T[h];
+        if (used + g > cap) continue;
+        t_hist.push_back(h), t_base.push_back(used), t_bits.push_back(ctab_T[h]), t_anyoff.push_back(anyw);
+        for (int r = 0; r < g; ++r) wg_team.push_back((int32_t)t_hist.size() - 1);
+        used += g;
+        anyw += enc.n_steps(h) / 32 + 2;
+        in_team[h] = 1;
+      }
+      for (int h : dense_c)
+        if (!in_team[h]) singles.push_back(h);
+    }
     HIP_TRY(hipEventRecord(ev0, stream));
-    HIP_TRY(launch_ctab(p, grid, stream));
+    if (!t_hist.empty()) {
+      const int nt = (int)t_hist.size(), g = (int)wg_team.size();
+      int lbmax = 0;
+      size_t anyw = 0;
+      for (int k = 0; k < nt; ++k) {
+        lbmax = std::max(lbmax, enc.live_max[t_hist[k]] - t_bits[k]);
+        anyw = std::max(anyw, (size_t)t_anyoff[k] + enc.n_steps(t_hist[k]) / 32 + 2);
+      }
+      const int mshift = std::max(0, lbmax - CTAB_LO);
+      const size_t meta = (size_t)g * 4 + (size_t)nt * 13 + 64;
+      HIP_TRY(d_ctmeta.ensure(meta));
+      std::vector<char> mb(meta, 0);
+      memcpy(mb.data(), wg_team.data(), (size_t)g * 4);
+      memcpy(mb.data() + (size_t)g * 4, t_base.data(), (size_t)nt * 4);
+      memcpy(mb.data() + (size_t)g * 4 + nt * 4, t_hist.data(), (size_t)nt * 4);
+      memcpy(mb.data() + (size_t)g * 4 + nt * 8, t_anyoff.data(), (size_t)nt * 4);
+      memcpy(mb.data() + (size_t)g * 4 + nt * 12, t_bits.data(), (size_t)nt);
+      HIP_TRY(hipMemcpyAsync(d_ctmeta.p, mb.data(), meta, hipMemcpyHostToDevice, stream));
+      HIP_TRY(d_ctmirror.ensure(((size_t)g * CT_MRING) << mshift << 3));
+      const size_t ctl_b = (size_t)g * 8 + anyw * 4 + (size_t)nt * 256 + 64;
+      HIP_TRY(d_ctctl.ensure(ctl_b));
+      HIP_TRY(hipMemsetAsync(d_ctctl.p, 0, ctl_b, stream));
+      CtabTeamParams tp{};
+      tp.c = p;
+      tp.n_teams = nt;
+      const char* mp = (const char*)d_ctmeta.p;
+      tp.wg_team = (const int32_t*)mp;
+      tp.team_base = (const int32_t*)(mp + (size_t)g * 4);
+      tp.team_hist = (const int32_t*)(mp + (size_t)g * 4 + nt * 4);
+      tp.team_any_off = (const int32_t*)(mp + (size_t)g * 4 + nt * 8);
+      tp.team_bits = (const int8_t*)(mp + (size_t)g * 4 + nt * 12);
+      char* cp = (char*)d_ctctl.p;
+      tp.flags = (unsigned long long*)cp;
+      tp.anyv = (uint32_t*)(cp + (size_t)g * 8);
+      tp.ctl = (unsigned*)(cp + (size_t)g * 8 + anyw * 4);
+      tp.abort = (int32_t*)(cp + (size_t)g * 8 + anyw * 4 + (size_t)nt * 256);
+      tp.mirror = d_ctmirror.as<uint64_t>();
+      tp.mshift = mshift;
+      tp.watchdog = 2000000000ull;  // 20 s
+      HIP_TRY(launch_ctab_team(tp, g, stream));
+      int32_t ab = 0;
+      HIP_TRY(hipMemcpyAsync(&ab, tp.abort, 4, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (ab) {
+        last_error = "counter tile-team watchdog fired";
+        return LC_E_INTERNAL;
+      }
+      if (debug())
+        for (int k = 0; k < nt; ++k)
+          fprintf(stderr, "[lincheck] ctab team: h=%d width=%d steps=%d tiles=%d (lb %d)\n", t_hist[k],
+                  enc.live_max[t_hist[k]], enc.n_steps(t_hist[k]), 1 << t_bits[k], enc.live_max[t_hist[k]] - t_bits[k]);
+    }
+    if (!singles.empty()) {
+      // the single-workgroup kernel's queue: its histories, heaviest first (as build_dense ordered them)
+      HIP_TRY(d_ctord.ensure(singles.size() * 4));
+      std::vector<int32_t> so;
+      std::vector<char> is_single(n, 0);
+      for (int h : singles) is_single[h] = 1;
+      const int32_t* hord = reinterpret_cast<const int32_t*>(hpack + o_ord) +
+                            (dense_b.size() + dense_w.size() + dense_x.size() + dense_m.size());
+      for (int i = 0; i < nc; ++i)
+        if (is_single[hord[i]]) so.push_back(hord[i]);
+      if (so.size() != singles.size()) so.assign(singles.begin(), singles.end());
+      HIP_TRY(hipMemcpyAsync(d_ctord.p, so.data(), so.size() * 4, hipMemcpyHostToDevice, stream));
+      CtabParams q = p;
+      q.n = (int)so.size();
+      q.order = d_ctord.as<int32_t>();
+      HIP_TRY(launch_ctab(q, std::min((int)so.size(), dgrid_c), stream));
+    }
+    const int grid = (int)wg_team.size() + std::min((int)singles.size(), dgrid_c);
     HIP_TRY(hipEventRecord(ev1, stream));
     const size_t need = (size_t)n * 32 + 16;
     if (hstage_bytes < need) {

@@ -73,6 +73,27 @@ def test_gpu_ctab_random_vs_oracle(pipe, monkeypatch):
     assert any(e["valid"] == 0 for e in exp) and any(e["valid"] == 1 for e in exp)
 
 
+@pytest.mark.parametrize("T,pipe", [("1", "3"), ("2", "3"), ("3", "3"), ("4", "3"), ("2", "0")])
+def test_gpu_ctab_teams_vs_oracle(T, pipe, monkeypatch):
+    """counter tile teams (ctab_team_kernel: one history's table split over
+    2^T workgroups by its top T slots, mirrors in HBM between tiles) forced from
+    width 9 on, T = 1..4, double- and single-buffered tiles: bit-exact with the oracle on random
+    histories (crashed ops, :fail reads, perturbed reads) and with the one-workgroup kernel."""
+    monkeypatch.setenv("LC_CTAB_TEAM_MINW", "9")
+    monkeypatch.setenv("LC_CTAB_TEAM_T", T)
+    monkeypatch.setenv("LC_CTAB_PIPE", pipe)
+    h = _mixed_counters(60, 7100 + int(T) + 10 * int(pipe), max_ops=300, max_clients=16, max_crash=3)
+    g = _lib.check(2, 0, h)
+    assert _ctab_count() == h.n_hist
+    exp = oracle.check_many("counter", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"team T={T}")
+    monkeypatch.setenv("LC_CTAB_TEAM", "0")
+    g1 = _lib.check(2, 0, h)
+    for key in ("valid", "fail_idx", "explored"):
+        assert np.array_equal(g[key], g1[key]), key
+
+
 def test_gpu_ctab_matches_grid_kernel(monkeypatch):
     """The same batch on the closure tables and on the grid kernel (LC_CTAB_MAXW=0)."""
     h = _mixed_counters(60, 47, max_ops=200)
