@@ -35,8 +35,10 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 4  /* 2: lc_failure_configs gained last_op / out_last_op; 3: LC_MODEL_LEADER;
-                            4: LC_H_ABORTED, statistics 34..38 (counter closure tables) */
+#define LC_ABI_VERSION 5  /* 2: lc_failure_configs gained last_op / out_last_op; 3: LC_MODEL_LEADER;
+                            4: LC_H_ABORTED, statistics 34..38 (counter closure tables);
+                            5: statistic 42 (counter tile teams), failure configs of histories
+                               on the HBM tables (no LC_E_CONFIGS for their width) */
 
 enum lc_model { LC_MODEL_CAS_REGISTER = 1, LC_MODEL_COUNTER = 2, LC_MODEL_LEADER = 3 };
 enum lc_valid { LC_INVALID = 0, LC_VALID = 1, LC_UNKNOWN = 2 };
@@ -225,8 +227,10 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  * 39..41 the closure-table kernels' slowest history: its microseconds from dequeue to end (device
  *    clock), its RETURN steps, its live width (a launch bound by one history's chain of steps
  *    lasts about that long)
+ * 42 counter histories decided by tile teams (ctab_team_kernel: one history's table over 2^T
+ *    workgroups, live width 17..24; counted in 34)
  */
-#define LC_STATS_N 42
+#define LC_STATS_N 43
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
 void lc_plan_destroy(lc_plan* p);
 

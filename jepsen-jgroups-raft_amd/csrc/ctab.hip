@@ -53,7 +53,8 @@ struct __attribute__((aligned(16))) CStep {
   int32_t req[32];           // per slot: requirement relative to init (CQ_UNC / CQ_NEVER)
   int32_t cq[32];            // per slot: EQ index base (k < 6: req - base - lo_min; k >= 6: + d_k)
   int8_t d[32];              // per slot: delta
-  int16_t sh[2][128];        // sums of the hi slots' deltas: slots 6..12 by w & 127, 13..19 by w >> 7
+  int16_t sh[3][128];        // sums of the hi slots' deltas: slots 6..12 by w & 127, 13..19 by
+                             // (w >> 7) & 127, 20..26 by w >> 14 (tile teams, to CTAB_TEAM_LMAX)
   uint64_t eq[64];           // EQ[v]: positions p with S_lo(p) - lo_min = v
 };
 
@@ -142,14 +143,14 @@ __device__ __forceinline__ void ct_decode(const CtabParams& p, StreamWin& sw, in
   __hip_atomic_fetch_or(&dst->eq[slo - lo_min], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   // hi sums: entries lane and lane + 64 of both halves
 #pragma unroll
-  for (int half = 0; half < 2; ++half)
+  for (int half = 0; half < 3; ++half)
 #pragma unroll
     for (int e2 = 0; e2 < 2; ++e2) {
       const int e = lane + 64 * e2;
       int32_t s = 0;
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
-        const int32_t dk = rdl(d, CTAB_LO + 7 * half + k);
+        const int32_t dk = CTAB_LO + 7 * half + k < 32 ? rdl(d, CTAB_LO + 7 * half + k) : 0;
         if ((e >> k) & 1) s += dk;
       }
       dst->sh[half][e] = (int16_t)s;
@@ -205,7 +206,7 @@ __device__ __forceinline__ uint64_t ct_word(const uint64_t* Bt, uint32_t w, cons
 #else
   auto pmark = [](int) {};
 #endif
-  const int s_hi = (int)st->sh[0][wg & 127u] + (int)st->sh[1][(wg >> 7) & 127u];
+  const int s_hi = (int)st->sh[0][wg & 127u] + (int)st->sh[1][(wg >> 7) & 127u] + (int)st->sh[2][(wg >> 14) & 127u];
   pmark(0);
   const bool jhi = j >= CTAB_LO;
   // (a tile team's j above the tile's local slots gives jh 0 here: that tile pulls it remotely)
@@ -807,7 +808,7 @@ __global__ void __launch_bounds__(CT_TEAM) ctab_team_kernel(CtabTeamParams tp) {
         pv[b] = (pl && ((pmask >> b) & 1u)) ? HbmTab::ld(mirror(rank ^ (1 << b), t) + mo + r) : 0ull;
       if (xs >= 0) X &= keep_lo;
       else if (fx) X = ct_x(tab(t - 1), w, 0u, jp, keep_lo);
-      const int s_hi = (int)st->sh[0][wg & 127u] + (int)st->sh[1][(wg >> 7) & 127u];
+      const int s_hi = (int)st->sh[0][wg & 127u] + (int)st->sh[1][(wg >> 7) & 127u] + (int)st->sh[2][(wg >> 14) & 127u];
       uint64_t R0 = 0;
 #pragma unroll
       for (int b = 0; b < CTAB_TEAM_MAXB; ++b)

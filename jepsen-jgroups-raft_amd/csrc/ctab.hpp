@@ -24,6 +24,8 @@ namespace lc {
 
 constexpr int CTAB_LO = 6;          // slots inside a table word
 constexpr int CTAB_LMAX = 20;       // widest table a workgroup holds in LDS (2^20 bits = 128 KiB)
+constexpr int CTAB_TEAM_LMAX = 24;  // widest table a tile team holds (the step header's 24 live bits;
+                                    // 64 tiles of 18 local slots)
 constexpr int CTAB_MAX_NINV = 31;   // invocations per step (2 stream words each, a 128-word window;
                                     // never binding: a step's invocations are live, <= CTAB_LMAX)
 constexpr int CTAB_DMAX = 10;       // |delta| of every op (EQ tables of 64 entries over 6 slots)
@@ -71,7 +73,7 @@ int ctab_grid_size();
 // from another tile was finished one super-layer earlier. One cooperative launch: every team's
 // workgroups are resident together.
 constexpr int CT_MRING = 64;  // mirror slots per tile (steps)
-constexpr int CTAB_TEAM_MAXB = 4;  // team slots (16 tiles)
+constexpr int CTAB_TEAM_MAXB = 6;  // team slots (64 tiles)
 struct CtabTeamParams {
   CtabParams c;                  // sbeg, nsteps, lmax, words, stream, status, fail_step, explored, stats, stamps
   int32_t n_teams;

@@ -166,13 +166,19 @@ struct lc_plan {
   // counter histories on closure tables (ctab.hip), heaviest first
   std::vector<int> dense_c;
   int dgrid_c = 0;
-  int ctab_maxw = CTAB_LMAX;  // LC_CTAB_MAXW (0: counters take the grid kernel, tests)
+  // LC_CTAB_MAXW (0: counters take the grid kernel, tests): widest counter on the closure tables;
+  // past CTAB_LMAX (one workgroup's LDS) only as a tile team, to CTAB_TEAM_LMAX
+  int ctab_maxw = CTAB_TEAM_LMAX;
   int ctab_pipe = 3;          // LC_CTAB_PIPE: bit 0 double-buffered tables, bit 1 chunks from an LDS counter
   // counter tile teams (ctab_team_kernel): LC_CTAB_TEAM=0 keeps every counter on one
   // workgroup; histories of live width >= LC_CTAB_TEAM_MINW get 2^T tiles, T = LC_CTAB_TEAM_T or,
-  // by default, width - 17 clamped to 1..3 (tiles of <= 17 local slots: 2^11 words, double-buffered)
-  int ctab_team = 1, ctab_team_minw = 16, ctab_team_t = 0;
+  // by default, width - 15 (tiles of 15 local slots: 2^9 words, double-buffered). r5e/r5f sweeps
+  // (one MI355X): c2c4 (width 20) 117 ms on one workgroup, 123 / 82 / 61 / 48 / 46 / 47 ms at
+  // T = 1..6; c5x 38.9 s -> 19.7 / 13.5 / 10.1 / 9.7 / 10.0 s at T = 2..6; c2c (width 16) 31.8 ms
+  // alone, 37-41 ms as a team (its super-layers are one pass of ~430 words: latency, not issue)
+  int ctab_team = 1, ctab_team_minw = 17, ctab_team_t = 0;
   std::vector<int8_t> ctab_T;  // per history: team slots (0: one workgroup)
+  std::vector<char> ctab_grid;  // per history: a counter the tables could not run (run_ctab)
   DevArray d_cstats;
   DevArray d_dpack, d_dwords, d_dqueue, d_dstatus, d_dfail, d_dexpl;
   DevArray d_dres;  // run_dense's results in one block: explored | status | fail | stats | abort | stamps
@@ -386,7 +392,7 @@ struct lc_plan {
       wide_stall_hist = atoi(e);
       wide_stall_wg = atoi(strchr(e, ':') + 1);
     }
-    if ((e = getenv("LC_CTAB_MAXW"))) ctab_maxw = std::max(0, std::min(atoi(e), CTAB_LMAX));
+    if ((e = getenv("LC_CTAB_MAXW"))) ctab_maxw = std::max(0, std::min(atoi(e), CTAB_TEAM_LMAX));
     if ((e = getenv("LC_CTAB_PIPE"))) ctab_pipe = atoi(e);
     if ((e = getenv("LC_CTAB_TEAM"))) ctab_team = atoi(e);
     if ((e = getenv("LC_CTAB_TEAM_MINW"))) ctab_team_minw = atoi(e);
@@ -427,8 +433,8 @@ struct lc_plan {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
-    ctab_maxw = CTAB_LMAX, ctab_pipe = 3, wide_watchdog_ms = 20000, wide_force_abort = false;
-    ctab_team = 1, ctab_team_minw = 16, ctab_team_t = 0;
+    ctab_maxw = CTAB_TEAM_LMAX, ctab_pipe = 3, wide_watchdog_ms = 20000, wide_force_abort = false;
+    ctab_team = 1, ctab_team_minw = 17, ctab_team_t = 0;
     wide_stall_hist = wide_stall_wg = -1;
     wide_from = 99, wide_lbits = DENSE_LMAX;
     dense_pipe = 217039, pipe_env = false, plan_off = false;
@@ -565,6 +571,7 @@ struct lc_plan {
     dense_ok.assign(n, 0);
     wide_ok.assign(n, 0);
     ctab_T.assign(n, 0);
+    ctab_grid.assign(n, 0);
     if ((int)wide_streams.size() < n) wide_streams.resize(n);
     dense_cost.assign(n, 0.0);
     dense_nw.assign(n, 0);
@@ -698,7 +705,7 @@ struct lc_plan {
     nst[h] = 0;
     lm[h] = 0;
     dense_ok[h] = 0;
-    bool ok = !v.err && v.live_max <= ctab_maxw;
+    bool ok = !v.err && v.live_max <= ctab_maxw && (v.live_max <= CTAB_LMAX || ctab_team);
     int64_t ni = 0;
     for (int64_t t = 0; t < v.n_steps && ok; ++t) {
       if (v.step_ninv[t] > CTAB_MAX_NINV) ok = false;
@@ -721,8 +728,13 @@ struct lc_plan {
     const int Lh = v.live_max;
     int T = 0;
     if (ctab_team && Lh >= ctab_team_minw)
-      T = ctab_team_t > 0 ? ctab_team_t : std::max(1, std::min(3, Lh - 17));
+      T = ctab_team_t > 0 ? ctab_team_t : std::max(1, std::min(CTAB_TEAM_MAXB, Lh - 15));
     if (Lh - T < CTAB_LO + 1) T = 0;
+    if (Lh > CTAB_LMAX && (T == 0 || Lh - T > CTAB_LO + 13)) {  // (tiles of <= 2^13 words)
+      dense_ok[h] = 0;
+      nst[h] = 0;
+      return false;
+    }
     ctab_T[h] = (int8_t)T;
     uint32_t pi[32];
     for (int k = 0; k < 32; ++k) pi[k] = (uint32_t)k;
@@ -788,7 +800,9 @@ struct lc_plan {
     dense_cost[h] = cost;
     dense_nw[h] = out - out0;
     *out = 0u;  // the terminator (no DENSE_OPW)
-    return !keep_inv_arrays;
+    // (a history wider than one workgroup's table keeps its invocation arrays: should its team
+    // not fit the launch, it takes the grid kernel)
+    return !keep_inv_arrays && Lh <= CTAB_LMAX;
   }
 
   int build_dense() {
@@ -1774,33 +1788,48 @@ struct lc_plan {
       HIP_TRY(hipMemsetAsync(d_dlhist.p, 0, 16 * 12 * 8, stream));
       p.prof = d_dlhist.as<unsigned long long>();
     }
-    // tile teams first (one cooperative launch, the widest histories while their workgroups fit),
-    // then every other counter history one per workgroup; both write the same result arrays
-    std::vector<int32_t> t_hist, t_base, t_anyoff, wg_team;
-    std::vector<int8_t> t_bits;
+    // tile teams first (cooperative launches, each as many teams as fit the chip, the heaviest
+    // histories first), then every other counter history one per workgroup; all write the same
+    // result arrays
     std::vector<int32_t> singles;
+    std::vector<std::vector<int>> team_launches;
+    int n_team_hist = 0;
     {
       const int cap = std::min(ctab_team_max_wgs(), 256);
-      int used = 0, anyw = 0;
       std::vector<int> cand;
       for (int h : dense_c)
-        if (ctab_T[h] > 0) cand.push_back(h);
+        if (ctab_T[h] > 0 && (1 << ctab_T[h]) <= cap) cand.push_back(h);
       std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return dense_cost[a] > dense_cost[b]; });
       std::vector<char> in_team(n, 0);
+      int used = cap;
       for (int h : cand) {
         const int g = 1 << ctab_T[h];
-        if (used + g > cap) continue;
-        t_hist.push_back(h), t_base.push_back(used), t_bits.push_back(ctab_T[h]), t_anyoff.push_back(anyw);
-        for (int r = 0; r < g; ++r) wg_team.push_back((int32_t)t_hist.size() - 1);
+        if (used + g > cap) team_launches.emplace_back(), used = 0;
+        team_launches.back().push_back(h);
         used += g;
-        anyw += enc.n_steps(h) / 32 + 2;
         in_team[h] = 1;
+        ++n_team_hist;
       }
       for (int h : dense_c)
-        if (!in_team[h]) singles.push_back(h);
+        if (!in_team[h]) {
+          if (enc.live_max[h] > CTAB_LMAX) ctab_grid[h] = 1;  // (no team: the grid kernel)
+          else singles.push_back(h);
+        }
     }
     HIP_TRY(hipEventRecord(ev0, stream));
-    if (!t_hist.empty()) {
+    int team_wgs = 0;
+    for (const std::vector<int>& hs : team_launches) {
+      std::vector<int32_t> t_hist, t_base, t_anyoff, wg_team;
+      std::vector<int8_t> t_bits;
+      int anyw_acc = 0;
+      for (int h : hs) {
+        const int g = 1 << ctab_T[h];
+        t_hist.push_back(h), t_base.push_back((int32_t)wg_team.size()), t_bits.push_back(ctab_T[h]);
+        t_anyoff.push_back(anyw_acc);
+        for (int r = 0; r < g; ++r) wg_team.push_back((int32_t)t_hist.size() - 1);
+        anyw_acc += enc.n_steps(h) / 32 + 2;
+      }
+      team_wgs = std::max(team_wgs, (int)wg_team.size());
       const int nt = (int)t_hist.size(), g = (int)wg_team.size();
       int lbmax = 0;
       size_t anyw = 0;
@@ -1842,7 +1871,7 @@ struct lc_plan {
       HIP_TRY(launch_ctab_team(tp, g, stream));
       int32_t ab = 0;
       HIP_TRY(hipMemcpyAsync(&ab, tp.abort, 4, hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
+      HIP_TRY(hipStreamSynchronize(stream));  // (the next launch reuses the team buffers)
       if (ab) {
         last_error = "counter tile-team watchdog fired";
         return LC_E_INTERNAL;
@@ -1869,7 +1898,7 @@ struct lc_plan {
       q.order = d_ctord.as<int32_t>();
       HIP_TRY(launch_ctab(q, std::min((int)so.size(), dgrid_c), stream));
     }
-    const int grid = (int)wg_team.size() + std::min((int)singles.size(), dgrid_c);
+    const int grid = team_wgs + std::min((int)singles.size(), dgrid_c);
     HIP_TRY(hipEventRecord(ev1, stream));
     const size_t need = (size_t)n * 32 + 16;
     if (hstage_bytes < need) {
@@ -1894,6 +1923,7 @@ struct lc_plan {
     *ms += t;
     double expl = 0;
     for (int h : dense_c) {
+      if (ctab_grid[h]) continue;
       status[h] = st[h], fail_step[h] = fs[h], explored[h] = ex[h];
       expl += (double)ex[h];
       note_chain(h, stamp[2 * h], stamp[2 * h + 1]);
@@ -1904,7 +1934,8 @@ struct lc_plan {
     stats[6] += (double)cs[0];
     stats[12] += nc;
     stats[13] += t;
-    stats[34] += nc;
+    stats[34] += nc - (int)std::count(ctab_grid.begin(), ctab_grid.end(), (char)1);
+    stats[42] += (double)n_team_hist;
     stats[35] += t;
     stats[36] += (double)cs[0] + nc;
     stats[37] += (double)cs[0];
@@ -2293,7 +2324,8 @@ struct lc_plan {
     }
     if (max_t == INT32_MAX && path == 0 && dense_on && !dense_c.empty()) {
       if ((rc = run_ctab(&ms))) return rc;
-      for (int h : dense_c) done[h] = 1;
+      for (int h : dense_c)
+        if (!ctab_grid[h]) done[h] = 1;
     }
     if (max_t == INT32_MAX && path == 0 && dense_on && !dense_wd.empty()) {
       bool ran = false;

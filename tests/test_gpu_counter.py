@@ -9,6 +9,7 @@ search — verdict, failing :index triple and explored count — to the oracle's
 import json
 import os
 import random
+import sys
 
 import numpy as np
 import pytest
@@ -40,6 +41,13 @@ def _fixture(name):
     if not os.path.exists(p):
         pytest.skip(f"{p} not pinned yet (tests/golden/pin_counter.py {name})")
     return json.load(open(p))
+
+
+def _live_width(h, k):
+    """Most calls pending at once in history k (crashed ones stay pending; :fail ones never enter)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools"))
+    from crash_ramp import width_of
+    return width_of(h.select([k]))
 
 
 def _ctab_count():
@@ -117,9 +125,12 @@ def test_gpu_ctab_init_value(init):
         _cmp(g, oracle.check_one("counter", h.select([k]), init_value=init), k, f"init={init}")
 
 
-def test_gpu_ctab_wide_deltas_and_widths_route_to_grid():
-    """Histories the tables do not take (|delta| > 10, wider than 20 live slots) go to the grid
-    kernel in the same call; every answer still matches the oracle."""
+@pytest.mark.parametrize("team", ["1", "0"])
+def test_gpu_ctab_wide_deltas_and_widths_route_to_grid(team, monkeypatch):
+    """Histories the tables do not take (|delta| > 10; wider than 20 live slots without tile
+    teams, LC_CTAB_TEAM=0) go to the grid kernel in the same call; every answer still matches
+    the oracle."""
+    monkeypatch.setenv("LC_CTAB_TEAM", team)
     big = synth.gen_counter(120, 5, 0.0, 77)
     big.v0 = np.where((big.f == 3) & (big.vflags == 1), big.v0 * 20, big.v0)  # adds of 0..80
     big = H.from_columns(big.index, big.process, big.type, big.f, big.v0, big.v1, big.vflags)
@@ -196,3 +207,29 @@ def test_gpu_ctab_c5x_full_size_vs_fixture():
     g = _lib.check(2, 0, h)
     assert _ctab_count() == 1
     assert int(g["valid"][0]) == fx["valid"] and int(g["explored"][0]) == fx["explored"]
+
+
+def _counter_ramp():
+    """Counter histories with K crashed ops (each a slot live for good): live widths 21..24, past
+    one workgroup's LDS table (20), each a few seconds of the oracle."""
+    hs = [synth.gen_counter(ops, cl, 0.0, 777 + k, n_crashed=k)
+          for ops, cl, k in ((400, 16, 8), (300, 16, 9), (300, 16, 7), (400, 14, 8), (350, 16, 9))]
+    hs += [synth.gen_counter(400, 16, 0.0, 7800 + t, n_crashed=7, invalid=True) for t in range(3)]
+    return H.concat(hs)
+
+
+def test_gpu_ctab_teams_past_20_slots_vs_oracle():
+    """counters wider than one workgroup's table (live width 21..24, the step
+    header's limit) on tile teams of 2^T workgroups (T = width - 15: 64 tiles at 24), bit-exact
+    with the oracle (verdict, failing :index triple, explored); no grid-kernel fallback."""
+    h = _counter_ramp()
+    widths = [_live_width(h, k) for k in range(h.n_hist)]
+    assert max(widths) >= 23 and min(widths) >= 21, widths
+    assert max(widths) <= 24, widths
+    g = _lib.check(2, 0, h)
+    st = _lib.check_stats()
+    assert int(st["ctab_team_histories"]) == h.n_hist and int(st["ctab_histories"]) == h.n_hist, st
+    exp = oracle.check_many("counter", h)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"counter width {widths[k]}")
+    assert any(e["valid"] == 0 for e in exp) and any(e["valid"] == 1 for e in exp)
