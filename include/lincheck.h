@@ -35,10 +35,11 @@
 extern "C" {
 #endif
 
-#define LC_ABI_VERSION 5  /* 2: lc_failure_configs gained last_op / out_last_op; 3: LC_MODEL_LEADER;
+#define LC_ABI_VERSION 6  /* 2: lc_failure_configs gained last_op / out_last_op; 3: LC_MODEL_LEADER;
                             4: LC_H_ABORTED, statistics 34..38 (counter closure tables);
                             5: statistic 42 (counter tile teams), failure configs of histories
-                               on the HBM tables (no LC_E_CONFIGS for their width) */
+                               on the HBM tables (no LC_E_CONFIGS for their width);
+                            6: HBM tables to live width 36 in slabs, statistic 43 */
 
 enum lc_model { LC_MODEL_CAS_REGISTER = 1, LC_MODEL_COUNTER = 2, LC_MODEL_LEADER = 3 };
 enum lc_valid { LC_INVALID = 0, LC_VALID = 1, LC_UNKNOWN = 2 };
@@ -219,7 +220,7 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  *    hipSetDevice, 22 streams/events/occupancy queries, 23 uploads, 24 dense step streams
  * 25..27 dense big kernel: frontier configs in, frontier configs out, configs explored
  * 28..30 the same for the dense wave (+ MID) kernel
- * 31 histories decided on closure tables in HBM (wide.hip: live width 25..35; counted in 12 too)
+ * 31 histories decided on closure tables in HBM (wide.hip: live width 25..36; counted in 12 too)
  * 32 their kernel's ms (part of 0 and 13)
  * 33 their algorithmic HBM bytes: per step and live word, its X, its pulls and its store (8 B each)
  * 34 counter histories decided on closure tables (ctab.hip; counted in 12 too)  35 their kernel's ms
@@ -229,8 +230,10 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  *    lasts about that long)
  * 42 counter histories decided by tile teams (ctab_team_kernel: one history's table over 2^T
  *    workgroups, live width 17..24; counted in 34)
+ * 43 slabs of the HBM tables' last launch (2^split: a slab holds <= 2^32 words, so width 36 has 2;
+ *    LC_WIDE_SPLIT asks for up to 8)
  */
-#define LC_STATS_N 43
+#define LC_STATS_N 44
 int32_t lc_plan_stats(lc_plan* p, double* stats, int32_t n);
 void lc_plan_destroy(lc_plan* p);
 

@@ -194,6 +194,7 @@ struct lc_plan {
   bool wide_force_abort = false;  // LC_WIDE_FORCE_ABORT=1 (tests): the abort word set before launch
   int wide_stall_hist = -1, wide_stall_wg = -1;  // LC_WIDE_STALL=h:wg (tests): a real barrier stall
   bool wide_pipe = true;  // LC_WIDE_PIPE=0: one step at a time (a grid barrier per popcount layer)
+  int wide_split = 0;     // LC_WIDE_SPLIT: at least this many split bits (2^split slabs; tests)
   // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
   // begin / step count / table width, and the queue order
   uint32_t* dp_stream = nullptr;
@@ -385,6 +386,7 @@ struct lc_plan {
     if ((e = getenv("LC_WIDE_MAXW"))) wide_maxw = std::max(0, std::min(atoi(e), WIDE_LMAX));
     if ((e = getenv("LC_WIDE_MINW"))) wide_minw = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_PIPE"))) wide_pipe = atoi(e) != 0;
+    if ((e = getenv("LC_WIDE_SPLIT"))) wide_split = std::max(0, std::min(atoi(e), WIDE_MAX_SPLIT));
     if ((e = getenv("LC_WIDE_GRID"))) wide_grid = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_WATCHDOG_MS")) && atoi(e) >= 0) wide_watchdog_ms = atoi(e);
     if ((e = getenv("LC_WIDE_FORCE_ABORT"))) wide_force_abort = atoi(e) != 0;
@@ -432,7 +434,7 @@ struct lc_plan {
   void reset_knobs() {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
-    wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0;
+    wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0, wide_split = 0;
     ctab_maxw = CTAB_TEAM_LMAX, ctab_pipe = 3, wide_watchdog_ms = 20000, wide_force_abort = false;
     ctab_team = 1, ctab_team_minw = 17, ctab_team_t = 0;
     wide_stall_hist = wide_stall_wg = -1;
@@ -606,7 +608,7 @@ struct lc_plan {
   // all), and records the tables' layout of its last launch
   int wide_stop = -1;
   bool wide_last_ranked = false, wide_ran = false;
-  int wide_last_hm = 0;
+  int wide_last_hm = 0, wide_last_split = 0;
   bool keep_inv_arrays = false;  // lc_failure_configs: its grid re-run needs every history's
   // returns true when h's step stream was built (its invocation arrays are then not needed)
   bool dense_sink(int h, const HistView& v) {
@@ -2032,6 +2034,7 @@ struct lc_plan {
     WideDumpParams d{};
     d.ranked = wide_last_ranked ? 1 : 0;
     d.Hm = wide_last_hm;
+    d.split = wide_last_split;
     // the dump: the frontier before step t_fail
     const int64_t cap = (int64_t)1 << 22;
     DevArray d_masks, d_states, d_cnt;
@@ -2070,7 +2073,7 @@ struct lc_plan {
     // the walk, one step back per round: tables of steps S - 1, S - 2 are in place
     int S = t_fail;
     DevArray d_hw, d_words;
-    std::vector<uint32_t> hw;
+    std::vector<uint64_t> hw;
     std::vector<uint64_t> words;
     for (int st = t_fail - 1; st >= 0 && !open.empty(); --st) {
       if (st < S - 2) {
@@ -2078,12 +2081,12 @@ struct lc_plan {
         if ((rc = run_to(S))) return rc;
       }
       hw.resize(open.size());
-      for (size_t k = 0; k < open.size(); ++k) hw[k] = (uint32_t)(cur[open[k]] >> 3);
-      HIP_TRY(d_hw.ensure(hw.size() * 4));
+      for (size_t k = 0; k < open.size(); ++k) hw[k] = cur[open[k]] >> 3;
+      HIP_TRY(d_hw.ensure(hw.size() * 8));
       HIP_TRY(d_words.ensure(hw.size() * 8));
-      HIP_TRY(hipMemcpy(d_hw.p, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(d_hw.p, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
       d.tab = table_of(st);
-      HIP_TRY(launch_wide_gather(d, d_hw.as<uint32_t>(), d_words.as<uint64_t>(), (int)hw.size(), stream));
+      HIP_TRY(launch_wide_gather(d, d_hw.as<uint64_t>(), d_words.as<uint64_t>(), (int)hw.size(), stream));
       words.resize(hw.size());
       HIP_TRY(hipMemcpyAsync(words.data(), d_words.p, words.size() * 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
@@ -2181,8 +2184,13 @@ struct lc_plan {
     p.nsteps = (const int32_t*)((char*)d_wmeta.p + 2 * m_sb);
     p.lmax = (const int8_t*)((char*)d_wmeta.p + 2 * m_sb + m_ns);
     // (the one-step kernel's prefix tables stop at WIDE_NOPIPE_LMAX: wider tables always pipeline)
-    p.pipe = wide_pipe || lmax > WIDE_NOPIPE_LMAX ? 1 : 0;
-    wide_last_ranked = p.pipe != 0, wide_last_hm = std::max(0, lmax - 3);
+    // slabs (§3.10): a slab's local index is 32-bit, so past 2^32 words the top hi bits split
+    // the table; LC_WIDE_SPLIT asks for more split bits (the rank split, tests), never leaving a
+    // slab without a hi bit of its own
+    const int hm = std::max(0, lmax - 3);
+    p.split = std::min(std::max(wide_split, hm - WIDE_SLAB_BITS), std::max(0, hm - 1));
+    p.pipe = wide_pipe || lmax > WIDE_NOPIPE_LMAX || p.split > 0 ? 1 : 0;
+    wide_last_ranked = p.pipe != 0, wide_last_hm = hm, wide_last_split = p.split;
     p.stream = d_wstream.as<uint32_t>();
     p.words = d_dwords.as<uint32_t>();
     p.tab = d_wtab.as<uint64_t>();
@@ -2237,6 +2245,7 @@ struct lc_plan {
     stats[13] += t;
     stats[31] += nwd;
     stats[32] += t;
+    stats[43] = std::max(stats[43], (double)(1 << p.split));
     // algorithmic bytes: every live word of every step read as X, pulled by its popcount-q
     // successors... counted from the reader: X (8 B) + popcount pulls (8 B each) + its store
     double alg = 0;

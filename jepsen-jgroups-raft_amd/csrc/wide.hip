@@ -39,7 +39,7 @@ constexpr int WWG = 1024;
 // 1024-thread workgroup holds a CU at 4)
 constexpr int WPWG = LC_WIDE_PWG;
 constexpr int WP_MINW = WPWG == 1024 ? 1 : LC_WIDE_MINW_EU;
-constexpr int WB = 33;  // binomials C(n, k) for n <= 32 (u32: C(32, 16) = 601,080,390)
+constexpr int WB = 34;  // binomials C(n, k) for n <= 33 (u32: C(33, 16) = 1,166,803,110)
 constexpr int WH = WIDE_LMAX - 3;  // most hi bits
 constexpr int WPRE = 513;          // per layer: prefix over <= 512 high parts, + the total
 
@@ -182,6 +182,15 @@ __device__ __forceinline__ uint64_t wide_pulls_ranked(const uint64_t* B, uint32_
       if (ix[u] != 0xffffffffu) R |= transfer(ops[bb[u] + 3], (foldm >> (bb[u] + 3)) & 1u, v[u]);
   }
   return R;
+}
+
+// ---- slabs (DESIGN.md §3.10 "Slabs"): the top `split` hi bits of a word w
+// pick its slab s = w >> Hl, Hl = Hm - split <= 32; inside the slab w is ranked over its low Hl
+// bits (wl) as above. A pull over a split bit reads the same local index in the neighbouring slab
+// (index - 2^b); every other access stays inside w's slab. split 0 is the single ranked table.
+__device__ __forceinline__ uint64_t slab_index(uint64_t w, int Hl, const uint32_t* bin, const uint32_t* off) {
+  const uint32_t wl = (uint32_t)(w & ((1ull << Hl) - 1ull));
+  return ((w >> Hl) << Hl) + off[__popc(wl)] + colex_rank(wl, bin);
 }
 
 __global__ void __launch_bounds__(WWG) wide_kernel(WideParams p) {
@@ -390,8 +399,8 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
   __shared__ uint32_t sBin[WB * WB];
   __shared__ uint32_t sLay[WIDE_LOW_BITS + 2];
   __shared__ WStep sRing[WRING];
-  __shared__ uint32_t sSeg[WRING + 1];  // running segments' first flat index (+ the total)
-  __shared__ uint32_t sOff[WH + 2];     // the ranked layout's layer offsets (colex_rank)
+  __shared__ uint64_t sSeg[WRING + 1];  // running segments' first flat index (+ the total)
+  __shared__ uint32_t sOff[WH + 2];     // the ranked layout's layer offsets inside a slab (colex_rank)
   __shared__ unsigned long long sRed;
   __shared__ int sAbort;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -411,10 +420,11 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
     for (int r = 0; r < tid; ++r) o += sBin[DENSE_WORD_BITS * WB + r];
     sLay[tid] = o;
   }
+  const int Hl = 63 - __clzll((long long)p.tab_words) - p.split;  // (tab_words = 2^Hm; a slab 2^Hl)
+  const uint64_t lmask = (1ull << Hl) - 1ull;
   if (tid <= WH + 1) {
-    const int Hm = 63 - __clzll((long long)p.tab_words);  // (tab_words = 2^Hm)
-    uint32_t o = 0;
-    for (int r = 0; r < tid && r <= Hm; ++r) o += sBin[Hm * WB + r];
+    uint32_t o = 0;  // (off[Hl + 1] = 2^Hl wraps at Hl = 32: never read)
+    for (int r = 0; r < tid && r <= Hl; ++r) o += sBin[Hl * WB + r];
     sOff[tid] = o;
   }
   // XCD-aware chunks: workgroups are dealt to the 8 XCDs round robin, so logical block
@@ -482,7 +492,7 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
       if (fail_t >= 0 || t_ret >= ns) break;
       // ---- this super-layer's segments: running step t in its layer q = s - start (C(H, q) words)
       if (tid <= WRING) {
-        uint32_t acc = 0;
+        uint64_t acc = 0;
         for (int t = t_ret; t < t_run && t - t_ret < tid; ++t) {
           const WStep& r = sRing[t % WRING];
           const int q = s - r.start;
@@ -491,16 +501,16 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
         sSeg[tid] = acc;
       }
       __syncthreads();
-      const uint32_t total = sSeg[t_run - t_ret];
+      const uint64_t total = sSeg[t_run - t_ret];
       uint32_t anyseg = 0;  // running steps (bit t - t_ret) in which this thread read a nonzero X
       for (int64_t g = gtid; g < (int64_t)total; g += gstride) {
         int si = 0;  // the segment holding g
-        while (si + 1 < t_run - t_ret && sSeg[si + 1] <= (uint32_t)g) ++si;
+        while (si + 1 < t_run - t_ret && sSeg[si + 1] <= (uint64_t)g) ++si;
         const int t = t_ret + si;
         const WStep& r = sRing[t % WRING];
         const int H = r.H, q = s - r.start;
         const int k = max(H < LC_WIDE_KLO ? H : LC_WIDE_KLO, H - WIDE_LOW_BITS), hb = H - k;
-        uint32_t gi = (uint32_t)g - sSeg[si];
+        uint32_t gi = (uint32_t)((uint64_t)g - sSeg[si]);  // (< C(33, 16) < 2^32)
         int pp = q - k > 0 ? q - k : 0;  // the high part's popcount: blocks of C(hb, p) C(k, q - p)
         for (;; ++pp) {
           const uint32_t blk = sBin[hb * WB + pp] * sBin[k * WB + (q - pp)];
@@ -509,26 +519,41 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
         }
         const uint32_t nlo = sBin[k * WB + (q - pp)];
         const uint32_t hi_i = gi / nlo, lo_i = gi - hi_i * nlo;
-        const uint32_t w = (hb ? (p.words[sLay[pp] + hi_i] << k) : 0u) | p.words[sLay[q - pp] + lo_i];
+        const uint64_t w = (hb ? (uint64_t)p.words[sLay[pp] + hi_i] << k : 0ull) | p.words[sLay[q - pp] + lo_i];
         const uint64_t live = r.live;
-        if ((uint64_t)w & ~(live >> 3)) continue;
+        if (w & ~(live >> 3)) continue;
         const uint64_t fresh = r.fresh, foldm = r.foldm;
         const int j = (int)r.j, jp = r.jp;
         uint64_t X = 0;
         uint32_t T0;
-        const uint32_t iw = sOff[q] + colex_rank(w, sBin, &T0);  // (|w| = q)
+        // w's slab (its first word sb) and its index inside it, over the slab's hi bits wl
+        const uint32_t wl = (uint32_t)(w & lmask);
+        const int ql = __popc(wl);
+        const uint64_t sb = w & ~lmask;
+        const uint64_t iw = sb + sOff[ql] + colex_rank(wl, sBin, &T0);
         if (!(w & (fresh >> 3))) {
           const uint64_t* Bp = tab(t - 1);
-          if (jp >= 3) X = HbmTab::ld(&Bp[sOff[q + 1] + colex_rank(w | (1u << (jp - 3)), sBin)]);
-          else if (jp >= 0) X = (HbmTab::ld(&Bp[iw]) & ~keep64(jp)) >> (1 << jp);
+          if (jp >= 3) {  // w + jp: in w's slab, or (a split bit) the same index one slab up
+            const int bp = jp - 3;
+            X = HbmTab::ld(&Bp[bp < Hl ? sb + sOff[ql + 1] + colex_rank(wl | (1u << bp), sBin) : iw + (1ull << bp)]);
+          } else if (jp >= 0) X = (HbmTab::ld(&Bp[iw]) & ~keep64(jp)) >> (1 << jp);
           else X = HbmTab::ld(&Bp[iw]);
 #pragma unroll
           for (int kk = 0; kk < 3; ++kk)
             if (fresh & (1u << kk)) X &= keep64(kk);
         }
         uint64_t* const B = tab(t);
-        uint64_t R = wide_pulls_ranked(B, w, j >= 3 ? 1u << (j - 3) : 0u, r.ops, foldm, sBin, q > 0 ? sOff[q - 1] : 0u, T0);
-        R = close_in_word(X, w, (uint32_t)live, j, r.ops, (uint32_t)foldm, R);
+        const int bj = j - 3;  // the returning slot's hi bit (j >= 3)
+        const bool hasj = j >= 3 && ((w >> bj) & 1ull);
+        uint64_t R = 0;
+        if (!hasj || bj < Hl)  // pulls over the slab's own bits (only j's when w holds j)
+          R = wide_pulls_ranked(B + sb, wl, hasj ? 1u << bj : 0u, r.ops, foldm, sBin, ql > 0 ? sOff[ql - 1] : 0u, T0);
+        // pulls over the split bits: the same local index in the slab without bit b
+        for (uint64_t sm = hasj ? (bj >= Hl ? 1ull << bj : 0ull) : w & ~lmask; sm; sm &= sm - 1) {
+          const int b = __builtin_ctzll(sm);
+          R |= transfer(r.ops[b + 3], (foldm >> (b + 3)) & 1u, HbmTab::ld(&B[iw - (1ull << b)]));
+        }
+        R = close_in_word(X, hasj ? 1u : 0u, (uint32_t)live, j >= 3 ? 3 : j, r.ops, (uint32_t)foldm, R);
         HbmTab::st(&B[iw], X | R);
         expl += (uint64_t)__popcll(R);
         if (t > 0) st_fout += (uint64_t)__popcll(X);
@@ -575,8 +600,8 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
       uint64_t nz = 0;
       for (int64_t w = gtid; w < nwt; w += gstride) {
         if ((uint64_t)w & ~(lv >> 3)) continue;
-        const uint32_t wr = pj >= 3 ? (uint32_t)w | (1u << (pj - 3)) : (uint32_t)w;
-        uint64_t X = HbmTab::ld(&Bl[sOff[__popc(wr)] + colex_rank(wr, sBin)]);
+        const uint64_t wr = pj >= 3 ? (uint64_t)w | (1ull << (pj - 3)) : (uint64_t)w;
+        uint64_t X = HbmTab::ld(&Bl[slab_index(wr, Hl, sBin, sOff)]);
         if (pj < 3) X = (X & ~keep64(pj)) >> (1 << pj);
         st_fout += (uint64_t)__popcll(X);
         nz |= X;
@@ -615,9 +640,9 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wide_pipe_kernel(WideParams p) 
 // stopped after step t - 1 (WideParams nsteps = the failing step t), tab(t - 1) holds step t - 1's
 // whole table; the frontier the failing RETURN saw is that table read through t - 1's returning
 // slot jp (the X of step t; its fresh slots are not live yet), dumped here config by config.
-__device__ __forceinline__ uint32_t dump_index(uint32_t w, const WideDumpParams& d, const uint32_t* bin,
+__device__ __forceinline__ uint64_t dump_index(uint64_t w, const WideDumpParams& d, const uint32_t* bin,
                                                const uint32_t* off) {
-  return d.ranked ? off[__popc(w)] + colex_rank(w, bin) : w;
+  return d.ranked ? slab_index(w, d.Hm - d.split, bin, off) : w;
 }
 
 __global__ void __launch_bounds__(256) wide_dump_kernel(WideDumpParams d) {
@@ -636,7 +661,7 @@ __global__ void __launch_bounds__(256) wide_dump_kernel(WideDumpParams d) {
   __syncthreads();
   if (tid <= WH + 1) {
     uint32_t o = 0;
-    for (int r = 0; r < tid && r <= d.Hm; ++r) o += sBin[d.Hm * WB + r];
+    for (int r = 0; r < tid && r <= d.Hm - d.split; ++r) o += sBin[(d.Hm - d.split) * WB + r];
     sOff[tid] = o;
   }
   __syncthreads();
@@ -644,7 +669,7 @@ __global__ void __launch_bounds__(256) wide_dump_kernel(WideDumpParams d) {
   const int64_t nwt = (int64_t)1 << (Lf > 3 ? Lf - 3 : 0);
   for (int64_t w = (int64_t)blockIdx.x * 256 + tid; w < nwt; w += (int64_t)gridDim.x * 256) {
     if ((uint64_t)w & ~(d.lv >> 3)) continue;
-    const uint32_t wr = d.jp >= 3 ? (uint32_t)w | (1u << (d.jp - 3)) : (uint32_t)w;
+    const uint64_t wr = d.jp >= 3 ? (uint64_t)w | (1ull << (d.jp - 3)) : (uint64_t)w;
     uint64_t X = HbmTab::ld(&d.tab[dump_index(wr, d, sBin, sOff)]);
     if (d.jp < 3) X = (X & ~keep64(d.jp)) >> (1 << d.jp);
     if (!X) continue;
@@ -660,7 +685,7 @@ __global__ void __launch_bounds__(256) wide_dump_kernel(WideDumpParams d) {
 }
 
 // out[i] = table word at the hi-bit word hw[i] (the ranked or natural index, as dump_index)
-__global__ void __launch_bounds__(256) wide_gather_kernel(WideDumpParams d, const uint32_t* hw, uint64_t* out, int n) {
+__global__ void __launch_bounds__(256) wide_gather_kernel(WideDumpParams d, const uint64_t* hw, uint64_t* out, int n) {
   __shared__ uint32_t sBin[WB * WB];
   __shared__ uint32_t sOff[WH + 2];
   const int tid = threadIdx.x;
@@ -676,7 +701,7 @@ __global__ void __launch_bounds__(256) wide_gather_kernel(WideDumpParams d, cons
   __syncthreads();
   if (tid <= WH + 1) {
     uint32_t o = 0;
-    for (int r = 0; r < tid && r <= d.Hm; ++r) o += sBin[d.Hm * WB + r];
+    for (int r = 0; r < tid && r <= d.Hm - d.split; ++r) o += sBin[(d.Hm - d.split) * WB + r];
     sOff[tid] = o;
   }
   __syncthreads();
@@ -709,7 +734,7 @@ hipError_t launch_wide_dump(const WideDumpParams& d, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_wide_gather(const WideDumpParams& d, const uint32_t* hw, uint64_t* out, int n, hipStream_t stream) {
+hipError_t launch_wide_gather(const WideDumpParams& d, const uint64_t* hw, uint64_t* out, int n, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(wide_gather_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, d, hw, out, n);
   return hipGetLastError();

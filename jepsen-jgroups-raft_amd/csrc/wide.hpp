@@ -14,9 +14,11 @@
 
 namespace lc {
 
-constexpr int WIDE_LMAX = 35;       // widest history: 2 tables of 2^32 words (64 GiB of the 288 GB HBM)
+constexpr int WIDE_LMAX = 36;       // widest history: 2 tables of 2^33 words (128 GiB of the 288 GB HBM)
+constexpr int WIDE_SLAB_BITS = 32;  // a slab holds at most 2^32 words (its local index is 32-bit)
+constexpr int WIDE_MAX_SPLIT = 3;   // at most 2^3 slabs (LC_WIDE_SPLIT, the rank split of §3.10)
 constexpr int WIDE_NOPIPE_LMAX = 31;  // the one-step-at-a-time kernel's layer prefix tables stop here
-constexpr int WIDE_OPS = 36;        // op-table entries per step (slots 0..34, + the pull loop's reads)
+constexpr int WIDE_OPS = 37;        // op-table entries per step (slots 0..35, + the pull loop's reads)
 constexpr int WIDE_MAX_NINV = 60;   // invocations per step (3 header words + 60 in a 64-lane read;
                                     // never binding: a step's invocations are live, <= WIDE_LMAX)
 constexpr int WIDE_LOW_BITS = 19;   // a layer's words = high part x low part from the sorted list
@@ -37,6 +39,9 @@ struct WideParams {
   const uint32_t* words;      // the DENSE_WORD_BITS-bit sorted word list (dense_word_list)
   uint64_t* tab;              // 2 tables of tab_words words each
   int64_t tab_words;
+  // the pipelined kernel's slabs: the top `split` hi bits of a word pick one of 2^split slabs of
+  // tab_words >> split words (<= 2^32), ranked inside the slab over the remaining hi bits
+  int32_t split;
   int32_t* status;            // [n] ST_VALID / ST_INVALID
   int32_t* fail_step;         // [n] the failing RETURN step (-1: none)
   unsigned long long* explored;  // [n] (zeroed before launch)
@@ -61,6 +66,7 @@ struct WideDumpParams {
   const uint64_t* tab;
   int32_t ranked;  // the pipelined kernel's layout (colex_rank), else word w at index w
   int32_t Hm;      // the table holds 2^Hm words
+  int32_t split;   // in 2^split slabs (ranked layout only)
   uint64_t lv;
   int32_t jp;
   int64_t cap;
@@ -72,7 +78,7 @@ struct WideDumpParams {
 hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream);
 hipError_t launch_wide_dump(const WideDumpParams& d, hipStream_t stream);
 // out[i] = the word of tab (as d: layout, Hm) at hi-bit word hw[i]
-hipError_t launch_wide_gather(const WideDumpParams& d, const uint32_t* hw, uint64_t* out, int n, hipStream_t stream);
+hipError_t launch_wide_gather(const WideDumpParams& d, const uint64_t* hw, uint64_t* out, int n, hipStream_t stream);
 int wide_grid_size(bool pipe);
 size_t wide_bar_bytes();
 

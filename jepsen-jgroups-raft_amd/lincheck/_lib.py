@@ -20,8 +20,8 @@ EXPORTS = ("lc_abi_version", "lc_device_count", "lc_check", "lc_release", "lc_ch
            "lc_bounds_plan_run", "lc_bounds_plan_destroy", "lc_part_create", "lc_part_info",
            "lc_part_step_begin", "lc_part_expand", "lc_part_pack", "lc_part_absorb",
            "lc_part_step_end", "lc_part_results", "lc_part_run", "lc_part_destroy", "lc_part_check")
-ABI_VERSION = 5
-STATS_N = 43
+ABI_VERSION = 6
+STATS_N = 44
 STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candidates",
                "frontier_out", "closure_new", "config_bytes", "alg_bytes", "workgroups",
                "spill_inserts", "dense_histories", "dense_ms", "dense_big_ms", "dense_wave_ms",
@@ -33,7 +33,7 @@ STATS_NAMES = ("kernel_ms", "launches", "steps", "phases", "frontier_in", "candi
                "wide_histories", "wide_ms", "wide_hbm_bytes",
                "ctab_histories", "ctab_ms", "ctab_frontier_in", "ctab_frontier_out", "ctab_explored",
                "slowest_history_us", "slowest_history_steps", "slowest_history_width",
-               "ctab_team_histories")
+               "ctab_team_histories", "wide_slabs")
 
 P = C.c_void_p
 I8P = C.POINTER(C.c_int8)

@@ -1236,6 +1236,90 @@ def test_gpu_wide_tables_past_31_slots():
             _check_configs_vs_oracle(h, f"wide w={w}")
 
 
+def _read_never_written(h, at_frac):
+    """h with its first :ok scalar read from entry at_frac * n on returning 7, a value the
+    generator never writes (its domain is 0..4): invalid from that read on."""
+    reads = [i for i in range(int(at_frac * h.n), h.n)
+             if h.type[i] == 1 and h.f[i] == 0 and h.vflags[i] == H.V_SCALAR]
+    v0 = h.v0.copy()
+    v0[reads[0]] = 7
+    return H.from_columns(h.index, h.process, h.type, h.f, v0, h.v1, h.vflags)
+
+
+@pytest.mark.parametrize("split", ["1", "2", "3"])
+def test_gpu_wide_slabs_vs_oracle(split, monkeypatch):
+    """the HBM tables split by their top `split` hi bits into 2^split slabs
+    (each ranked over its own hi bits; pulls over a split bit read the neighbouring slab), forced
+    with LC_WIDE_SPLIT on every history from width 12 on: random valid and invalid histories and
+    16-client ones with crashed ops against the oracle, and one failure report as sets."""
+    monkeypatch.setenv("LC_WIDE_MINW", "12")
+    monkeypatch.setenv("LC_WIDE_SPLIT", split)
+    hs = [synth.gen_register(300, 16, 0.01, 52100 + t, n_crashed=2 + t) for t in range(6)]
+    hs += [synth.gen_register(200, 12, 0.05, 52200 + t) for t in range(6)]
+    h = H.concat([_read_never_written(x, 0.3 + 0.1 * (t % 5)) if t % 2 else x for t, x in enumerate(hs)])
+    widths = [_live_width(h, k) for k in range(h.n_hist)]
+    g = _lib.check(1, 0, h)
+    st = _lib.check_stats()
+    assert st["wide_histories"] == sum(1 for w in widths if w >= 12) > 0
+    assert int(st["wide_slabs"]) == 1 << int(split)
+    exp = oracle.check_many("cas-register", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"slabs split={split} w={widths[k]}")
+    bad = [k for k in range(h.n_hist) if exp[k]["valid"] == 0 and widths[k] >= 12]
+    assert bad
+    one = h.select([min(bad, key=lambda k: exp[k]["explored"])])
+    g1 = _lib.check(1, 0, one)
+    assert int(g1["valid"][0]) == 0 and int(_lib.check_stats()["wide_slabs"]) == 1 << int(split)
+    _check_configs_vs_oracle(one, f"slabs split={split}")
+
+
+def test_gpu_wide_slabs_match_one_table_on_the_crash_ramp():
+    """The slab split (2, 4, 8 slabs: the table's rank split multiplexed on one device) gives the
+    single table's verdict, failing op and explored count on the crash ramp's real wide frontiers
+    (K = 13..18: widths 27..33, 7 G to 390 G configs)."""
+    for k in (13, 14, 16, 18):
+        h = synth.gen_register(2000, 16, 0.002, 0x5EED4000 + k, n_crashed=k)
+        a = _lib.check(1, 0, h)
+        st = _lib.check_stats()
+        assert st["wide_histories"] == 1 and int(st["wide_slabs"]) == 1, (k, st["wide_slabs"])
+        for split in ("1", "2", "3"):
+            os.environ["LC_WIDE_SPLIT"] = split
+            try:
+                b = _lib.check(1, 0, h)
+                st = _lib.check_stats()
+            finally:
+                del os.environ["LC_WIDE_SPLIT"]
+            assert st["wide_histories"] == 1 and int(st["wide_slabs"]) == 1 << int(split)
+            for key in ("valid", "fail_idx", "fail_inv", "prev_ok", "explored"):
+                assert int(a[key][0]) == int(b[key][0]), (k, split, key, a[key][0], b[key][0])
+
+
+def test_gpu_wide_tables_at_width_36():
+    """r5: live width 36 (2 x 2^33 words = 128 GiB, two slabs of 2^32 words per table: a slab's
+    index is 32-bit): a 12-op base with 34 calls pending throughout that can never apply, valid
+    and with a read of a value never written, against the oracle."""
+    for n, bad, seed in ((34, False, 57100), (34, True, 57101)):
+        base = synth.gen_register(12, 2, 0.0, seed)
+        if bad:
+            reads = [i for i in range(base.n) if base.type[i] == 1 and base.f[i] == 0 and base.vflags[i] == H.V_SCALAR]
+            assert reads
+            v0 = base.v0.copy()
+            v0[reads[-1]] = 7
+            base = H.from_columns(base.index, base.process, base.type, base.f, v0, base.v1, base.vflags)
+        h = _with_never_ops(base, n)
+        w = _live_width(h, 0)
+        assert w == 36, w
+        g = _lib.check(1, 0, h)
+        st = _lib.check_stats()
+        assert st["wide_histories"] == 1 and int(st["wide_slabs"]) == 2, (w, st["wide_slabs"])
+        e = oracle.check_one("cas-register", h)
+        assert e["valid"] == (0 if bad else 1)
+        _cmp(g, e, 0, f"wide w={w}")
+        assert int(g["explored"][0]) == oracle.check_one("cas-register", base)["explored"]
+        if bad:
+            _check_configs_vs_oracle(h, f"wide w={w}")
+
+
 def test_gpu_wide_watchdog_abort_is_unknown(monkeypatch):
     """when the HBM tables' grid barrier watchdog fires (its abort word forced here
     with LC_WIDE_FORCE_ABORT=1, as a fired watchdog leaves it) the call still succeeds: the wide

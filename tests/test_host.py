@@ -26,7 +26,7 @@ def test_library_exports_every_symbol():
     L = _lib.load()
     for s in _declared():
         assert hasattr(L, s), s
-    assert L.lc_abi_version() == _lib.ABI_VERSION == 5
+    assert L.lc_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_no_device_fails_loudly():

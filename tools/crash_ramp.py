@@ -139,7 +139,7 @@ def main():
     ap.add_argument("--part", action="store_true")
     ap.add_argument("--part-cap", type=int, default=0, help="lc_part_check capacity_log2 (0: default)")
     a = ap.parse_args()
-    ks = [int(x) for x in a.crashed.split(",") if x]
+    ks = [int(x) for x in a.crashed.replace("+", ",").split(",") if x]  # ("+": tools/run.sh splits commas)
     rows = {}
     for k in ks:
         h = make(a.ops, a.clients, k)
