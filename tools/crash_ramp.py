@@ -35,8 +35,15 @@ sys.path.insert(0, ROOT)
 SEED0 = 0x5EED4000  # SURVEY §8(d) seeds: config 4
 
 
-def make(ops: int, clients: int, k: int):
+MODEL = "cas-register"  # --model counter: the counter workload's ramp
+
+
+def make(ops: int, clients: int, k: int, model: str = "cas-register"):
+    """K crashed ops in the first 20 %: write/cas for a register; for a counter the timed-out
+    add / *-and-get ops of counter.clj:118-119,126-127 (client.clj:52-63 reports them :info)."""
     from lincheck import synth
+    if model == "counter":
+        return synth.gen_counter(ops, clients, 0.0, SEED0 + 0x100 + k, n_crashed=k, crash_span=0.2)
     return synth.gen_register(ops, clients, 0.002, SEED0 + k, n_crashed=k)
 
 
@@ -67,25 +74,28 @@ def width_of(h) -> int:
     return best
 
 
-def cpu_leg(ops, clients, k, q):
+def cpu_leg(ops, clients, k, model, q):
     from oracle import oracle
-    h = make(ops, clients, k)
+    h = make(ops, clients, k, model)
     t = time.perf_counter()
-    r = oracle.check_one("cas-register", h)
+    r = oracle.check_one(model, h)
     q.put({"wall_s": time.perf_counter() - t, "valid": int(r["valid"]), "explored": int(r["explored"]),
            "max_frontier": int(r.get("max_frontier", -1))})
 
 
-def gpu_leg(ops, clients, k, part, part_cap, q):
+def gpu_leg(ops, clients, k, part, part_cap, model, q):
     from lincheck import _lib
-    h = make(ops, clients, k)
+    h = make(ops, clients, k, model)
+    kind = _lib.MODEL_KIND[model]
     out = {}
     t = time.perf_counter()
-    r = _lib.check(1, 0, h)
+    r = _lib.check(kind, 0, h)
     out["lc_check"] = {"wall_s": time.perf_counter() - t, "valid": int(r["valid"][0]),
                        "explored": int(r["explored"][0]), "err": int(r["err"][0])}
     st = _lib.check_stats()
     out["lc_check"]["path"] = ("wide (HBM tables)" if st.get("wide_histories", 0) > 0
+                               else "counter tile team" if st.get("ctab_team_histories", 0) > 0
+                               else "counter tables" if st.get("ctab_histories", 0) > 0
                                else "dense" if st.get("dense_histories", 0) > 0 else "grid")
     out["lc_check"]["kernel_ms"] = st.get("kernel_ms")
     if st.get("wide_histories", 0) > 0:  # HBM-table kernel: algorithmic bytes / its time vs 8 TB/s
@@ -94,7 +104,7 @@ def gpu_leg(ops, clients, k, part, part_cap, q):
         out["lc_check"]["wide_alg_gbps"] = st["wide_hbm_bytes"] / st["wide_ms"] / 1e6 if st["wide_ms"] else None
     if out["lc_check"]["wall_s"] < 30:  # a second (warm) run: the device's first-use cost is gone
         t = time.perf_counter()
-        _lib.check(1, 0, h)
+        _lib.check(kind, 0, h)
         out["lc_check"]["wall_warm_s"] = time.perf_counter() - t
     if part:
         t = time.perf_counter()
@@ -138,22 +148,23 @@ def main():
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--part", action="store_true")
     ap.add_argument("--part-cap", type=int, default=0, help="lc_part_check capacity_log2 (0: default)")
+    ap.add_argument("--model", default="cas-register", choices=("cas-register", "counter"))
     a = ap.parse_args()
     ks = [int(x) for x in a.crashed.replace("+", ",").split(",") if x]  # ("+": tools/run.sh splits commas)
     rows = {}
     for k in ks:
-        h = make(a.ops, a.clients, k)
-        rows[k] = {"crashed": k, "ops": a.ops, "clients": a.clients, "width": width_of(h),
+        h = make(a.ops, a.clients, k, a.model)
+        rows[k] = {"model": a.model, "crashed": k, "ops": a.ops, "clients": a.clients, "width": width_of(h),
                    "entries": int(h.n)}
     if not a.no_cpu:  # every CPU leg first: nothing in this process has touched the GPU yet
         for k in ks:  # (stops at the first K past the limit: where the CPU side breaks)
-            rows[k]["cpu_oracle_1thread"] = run_child(cpu_leg, (a.ops, a.clients, k), a.cpu_timeout)
+            rows[k]["cpu_oracle_1thread"] = run_child(cpu_leg, (a.ops, a.clients, k, a.model), a.cpu_timeout)
             print(f"[ramp] K={k} cpu {rows[k]['cpu_oracle_1thread']}", file=sys.stderr, flush=True)
             if "timeout_s" in rows[k]["cpu_oracle_1thread"]:
                 break
     if not a.no_gpu:
         for k in ks:
-            rows[k]["gpu"] = run_child(gpu_leg, (a.ops, a.clients, k, a.part, a.part_cap), a.gpu_timeout)
+            rows[k]["gpu"] = run_child(gpu_leg, (a.ops, a.clients, k, a.part, a.part_cap, a.model), a.gpu_timeout)
             print(f"[ramp] K={k} gpu {rows[k]['gpu']}", file=sys.stderr, flush=True)
             if "timeout_s" in rows[k]["gpu"] or "error" in rows[k]["gpu"]:
                 break
