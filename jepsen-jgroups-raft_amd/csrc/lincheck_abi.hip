@@ -195,6 +195,9 @@ struct lc_plan {
   int wide_stall_hist = -1, wide_stall_wg = -1;  // LC_WIDE_STALL=h:wg (tests): a real barrier stall
   bool wide_pipe = true;  // LC_WIDE_PIPE=0: one step at a time (a grid barrier per popcount layer)
   int wide_split = 0;     // LC_WIDE_SPLIT: at least this many split bits (2^split slabs; tests)
+  // counters on the HBM tables (wctr_pipe_kernel, §3.13): widths past the tile teams up to
+  // LC_WCTR_MAXW (0: off, they take the grid kernel); LC_WCTR_MINW routes narrower ones (tests)
+  int wctr_maxw = WCTR_LMAX, wctr_minw = 0;
   // the dense kernels' inputs inside d_dpack (one upload): step streams, per-history stream
   // begin / step count / table width, and the queue order
   uint32_t* dp_stream = nullptr;
@@ -387,6 +390,8 @@ struct lc_plan {
     if ((e = getenv("LC_WIDE_MINW"))) wide_minw = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_PIPE"))) wide_pipe = atoi(e) != 0;
     if ((e = getenv("LC_WIDE_SPLIT"))) wide_split = std::max(0, std::min(atoi(e), WIDE_MAX_SPLIT));
+    if ((e = getenv("LC_WCTR_MAXW"))) wctr_maxw = std::max(0, std::min(atoi(e), WCTR_LMAX));
+    if ((e = getenv("LC_WCTR_MINW"))) wctr_minw = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_GRID"))) wide_grid = std::max(0, atoi(e));
     if ((e = getenv("LC_WIDE_WATCHDOG_MS")) && atoi(e) >= 0) wide_watchdog_ms = atoi(e);
     if ((e = getenv("LC_WIDE_FORCE_ABORT"))) wide_force_abort = atoi(e) != 0;
@@ -435,6 +440,7 @@ struct lc_plan {
     path = 0;
     tile_cap = 256, dense_maxw = DENSE_WIDE_LMAX, tile_lbits = DENSE_LMAX;
     wide_maxw = WIDE_LMAX, wide_minw = 0, wide_pipe = true, wide_grid = 0, wide_split = 0;
+    wctr_maxw = WCTR_LMAX, wctr_minw = 0;
     ctab_maxw = CTAB_TEAM_LMAX, ctab_pipe = 3, wide_watchdog_ms = 20000, wide_force_abort = false;
     ctab_team = 1, ctab_team_minw = 17, ctab_team_t = 0;
     wide_stall_hist = wide_stall_wg = -1;
@@ -694,6 +700,57 @@ struct lc_plan {
     wide_ok[h] = 1;
   }
 
+  // A wide counter history's step stream (wide.hip's counter format: three header words, then
+  // ctab.hpp's two words per invocation), into its own buffer as wide_sink's.
+  void wctr_sink(int h, const HistView& v) {
+    std::vector<uint32_t>& out = wide_streams[h];
+    out.clear();
+    const int64_t init = enc.init_value;
+    uint64_t live = 0;
+    int64_t q = 0;
+    for (int64_t t = 0; t < v.n_steps; ++t) {
+      if (t > 0) live &= ~(1ull << v.step_slot[t - 1]);
+      const int64_t q1 = q + v.step_ninv[t];
+      for (int64_t k = q; k < q1; ++k) live |= 1ull << v.inv_slot[k];
+      out.push_back((uint32_t)(live & 0x7fffffffu));
+      out.push_back((uint32_t)(live >> 31) & 0x7fffffffu);
+      out.push_back((uint32_t)v.step_slot[t]);
+      for (int64_t k = q; k < q1; ++k) {
+        uint32_t fl = 0;
+        int64_t req = 0;
+        counter_req(v.inv_kind[k], v.inv_a[k], v.inv_b[k], init, fl, req);
+        const int64_t delta = (v.inv_kind[k] & C_SUB) ? -v.inv_b[k] : v.inv_b[k];
+        out.push_back((uint32_t)v.inv_slot[k] | (fl << 8) | ((uint32_t)(uint8_t)(int8_t)delta << 16) | DENSE_OPW);
+        out.push_back(((uint32_t)(req + CTAB_REQ_BIAS) & 0x3fffffffu) | DENSE_OPW);
+      }
+      q = q1;
+    }
+    out.push_back(0u);
+    wide_ok[h] = 1;
+  }
+
+  // CounterModel.step's requirement of one op (counter.clj:102-127), relative to the initial
+  // value: a read of v needs v; an :ok *-and-get [d new] needs new - d (or new + d); flags CT_UNC
+  // (steps from any config) / CT_NEVER (from none: a pre- and post-condition that disagree, or a
+  // value out of the int32 range no config reaches)
+  static void counter_req(uint8_t kind, int64_t a, int64_t b, int64_t init, uint32_t& fl, int64_t& req) {
+    const int64_t delta = (kind & C_SUB) ? -b : b;
+    fl = 0;
+    req = 0;
+    if (!(kind & (C_PRE_EQ | C_POST_EQ))) {
+      fl = CT_UNC;
+      return;
+    }
+    int64_t r_pre = 0, r_post = 0;
+    bool never = false;
+    if (kind & C_PRE_EQ) never |= __builtin_sub_overflow(a, init, &r_pre);
+    if (kind & C_POST_EQ) never |= __builtin_sub_overflow(a, init, &r_post) || __builtin_sub_overflow(r_post, delta, &r_post);
+    req = (kind & C_PRE_EQ) ? r_pre : r_post;
+    if ((kind & C_PRE_EQ) && (kind & C_POST_EQ) && r_pre != r_post) never = true;
+    if (req >= CTAB_REQ_BIAS || req < -CTAB_REQ_BIAS) never = true;
+    if (never) fl = CT_NEVER, req = 0;
+  }
+
   // A counter history's step stream for the closure tables (ctab.hpp): each op as its delta and
   // the value, relative to the initial one, the counter must hold before it (CounterModel.step,
   // counter.clj:102-127: a read of v needs v; an :ok *-and-get [d new] needs new - d, or new + d
@@ -707,19 +764,26 @@ struct lc_plan {
     nst[h] = 0;
     lm[h] = 0;
     dense_ok[h] = 0;
-    bool ok = !v.err && v.live_max <= ctab_maxw && (v.live_max <= CTAB_LMAX || ctab_team);
-    int64_t ni = 0;
-    for (int64_t t = 0; t < v.n_steps && ok; ++t) {
-      if (v.step_ninv[t] > CTAB_MAX_NINV) ok = false;
-      ni += v.step_ninv[t];
-    }
+    // the counter tables' conditions on the ops (either layout): deltas within the EQ range, their
+    // absolute sum bounded, no leader ops, a step's invocations within the decoder's window
+    bool elig = !v.err;
+    int64_t ni = 0, max_ninv = 0;
+    for (int64_t t = 0; t < v.n_steps; ++t) ni += v.step_ninv[t], max_ninv = std::max(max_ninv, v.step_ninv[t]);
     int64_t dsum = 0;
-    for (int64_t k = 0; k < ni && ok; ++k) {
+    for (int64_t k = 0; k < ni && elig; ++k) {
       const int64_t d = v.inv_b[k];
-      if ((v.inv_kind[k] & C_LEADER) || d > CTAB_DMAX || d < -CTAB_DMAX) ok = false;
+      if ((v.inv_kind[k] & C_LEADER) || d > CTAB_DMAX || d < -CTAB_DMAX) elig = false;
       dsum += d < 0 ? -d : d;
     }
-    if (!ok || dsum >= CTAB_SUM_MAX) return false;
+    if (!elig || dsum >= CTAB_SUM_MAX) return false;
+    // past the tile teams (or from LC_WCTR_MINW on, tests): the HBM tables (§3.13)
+    const int cmin = wctr_minw > 0 ? wctr_minw : CTAB_TEAM_LMAX + 1;
+    if (v.live_max >= cmin && v.live_max <= wctr_maxw && max_ninv <= WCTR_MAX_NINV) {
+      wctr_sink(h, v);
+      return false;  // (its invocation arrays stay: lc_failure_configs re-runs it on the grid kernel)
+    }
+    const bool ok = v.live_max <= ctab_maxw && (v.live_max <= CTAB_LMAX || ctab_team) && max_ninv <= CTAB_MAX_NINV;
+    if (!ok) return false;
     dense_ok[h] = 1;
     nst[h] = (int32_t)v.n_steps;
     lm[h] = (int8_t)std::max(1, v.live_max);
@@ -777,21 +841,10 @@ struct lc_plan {
       *out++ = relabel(live) | (pi[v.step_slot[t]] << DENSE_J_SHIFT);
       for (int64_t k = q; k < q1; ++k) {
         const uint8_t kind = v.inv_kind[k];
-        const int64_t a = v.inv_a[k], delta = (kind & C_SUB) ? -v.inv_b[k] : v.inv_b[k];
+        const int64_t delta = (kind & C_SUB) ? -v.inv_b[k] : v.inv_b[k];
         uint32_t fl = 0;
         int64_t req = 0;
-        if (!(kind & (C_PRE_EQ | C_POST_EQ))) {
-          fl = CT_UNC;
-        } else {
-          int64_t r_pre = 0, r_post = 0;
-          bool never = false;
-          if (kind & C_PRE_EQ) never |= __builtin_sub_overflow(a, init, &r_pre);
-          if (kind & C_POST_EQ) never |= __builtin_sub_overflow(a, init, &r_post) || __builtin_sub_overflow(r_post, delta, &r_post);
-          req = (kind & C_PRE_EQ) ? r_pre : r_post;
-          if ((kind & C_PRE_EQ) && (kind & C_POST_EQ) && r_pre != r_post) never = true;
-          if (req >= CTAB_REQ_BIAS || req < -CTAB_REQ_BIAS) never = true;  // no config reaches it
-          if (never) fl = CT_NEVER, req = 0;
-        }
+        counter_req(kind, v.inv_a[k], v.inv_b[k], init, fl, req);
         *out++ = pi[v.inv_slot[k]] | (fl << 8) | ((uint32_t)(uint8_t)(int8_t)delta << 16) | DENSE_OPW;
         *out++ = ((uint32_t)(req + CTAB_REQ_BIAS) & 0x3fffffffu) | DENSE_OPW;
       }
@@ -2129,7 +2182,134 @@ struct lc_plan {
   // The wide histories (tables in HBM), one persistent launch over the whole GPU, one history
   // after another. `ran` stays false when the two tables do not fit the device (they then take
   // the grid kernel, as before).
+  // Counter histories on the HBM tables (wctr_pipe_kernel, §3.13): run_wide's launch with the
+  // counter layout (2^(lmax - 6) words per table, no slabs) and the counter stream format.
+  int run_wctr(float* ms, bool& ran) {
+    const int nwd = (int)dense_wd.size();
+    std::vector<int64_t> sbeg(nwd), aoff(nwd);
+    std::vector<int32_t> nst(nwd);
+    std::vector<int8_t> lmx(nwd);
+    std::vector<uint32_t> words;
+    int lmax = 0;
+    int64_t abits = 0;
+    for (int i = 0; i < nwd; ++i) {
+      const int h = dense_wd[i];
+      sbeg[i] = (int64_t)words.size();
+      nst[i] = enc.n_steps(h);
+      lmx[i] = (int8_t)enc.live_max[h];
+      lmax = std::max(lmax, (int)enc.live_max[h]);
+      words.insert(words.end(), wide_streams[h].begin(), wide_streams[h].end());
+      aoff[i] = abits, abits += nst[i] / 32 + 1;
+    }
+    words.resize(words.size() + 64, 0u);  // the decoder reads a 64-word window
+    if (lmax > WCTR_LMAX) {
+      last_error = "wide counter tables: a history wider than WCTR_LMAX";
+      return LC_E_INTERNAL;
+    }
+    const int64_t tw = (int64_t)1 << std::max(0, lmax - 6);
+    if (d_wtab.ensure((size_t)tw * 16) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;  // (the tables do not fit: the grid kernel)
+    }
+    int rc;
+    if ((rc = upload(d_wstream, words))) return rc;
+    if (!d_dwords.p) {
+      std::vector<uint32_t> wl(1u << DENSE_WORD_BITS);
+      dense_word_list(DENSE_WORD_BITS, wl.data());
+      if ((rc = upload(d_dwords, wl))) return rc;
+    }
+    const size_t m_sb = (size_t)nwd * 8, m_ns = (size_t)nwd * 4;
+    HIP_TRY(d_wmeta.ensure(2 * m_sb + m_ns + (size_t)nwd + 8));
+    HIP_TRY(hipMemcpy(d_wmeta.p, sbeg.data(), m_sb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((char*)d_wmeta.p + m_sb, aoff.data(), m_sb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((char*)d_wmeta.p + 2 * m_sb, nst.data(), m_ns, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((char*)d_wmeta.p + 2 * m_sb + m_ns, lmx.data(), (size_t)nwd, hipMemcpyHostToDevice));
+    const size_t r_bytes = (size_t)nwd * 24 + 32 + (size_t)abits * 4;
+    HIP_TRY(d_wres.ensure(r_bytes));
+    HIP_TRY(d_wbar.ensure(wide_bar_bytes() + 8));
+    HIP_TRY(hipMemsetAsync(d_wres.p, 0, r_bytes, stream));
+    HIP_TRY(hipMemsetAsync(d_wbar.p, 0, wide_bar_bytes() + 8, stream));
+    WideParams p{};
+    p.n = nwd;
+    p.sbeg = (const int64_t*)d_wmeta.p;
+    p.anyv_off = (const int64_t*)((char*)d_wmeta.p + m_sb);
+    p.nsteps = (const int32_t*)((char*)d_wmeta.p + 2 * m_sb);
+    p.lmax = (const int8_t*)((char*)d_wmeta.p + 2 * m_sb + m_ns);
+    p.pipe = 1;
+    p.stream = d_wstream.as<uint32_t>();
+    p.words = d_dwords.as<uint32_t>();
+    p.tab = d_wtab.as<uint64_t>();
+    p.tab_words = tw;
+    unsigned long long* const rex = d_wres.as<unsigned long long>();
+    p.explored = rex;
+    p.any = rex + nwd;
+    p.status = (int32_t*)(rex + 2 * nwd);
+    p.fail_step = p.status + nwd;
+    p.stats = (unsigned long long*)(p.fail_step + nwd);
+    p.anyv = (uint32_t*)(p.stats + 4);
+    p.bar = d_wbar.as<unsigned>();
+    p.abort = (int32_t*)((char*)d_wbar.p + wide_bar_bytes());
+    p.watchdog = (uint64_t)wide_watchdog_ms * 100000ull;
+    const int gmax = wctr_grid_size();
+    const int grid = wide_grid > 0 ? std::min(wide_grid, gmax) : gmax;
+    if (grid < 1) {
+      last_error = "wide counter kernel: no resident workgroups";
+      return LC_E_INTERNAL;
+    }
+    HIP_TRY(hipEventRecord(ev0, stream));
+    HIP_TRY(launch_wctr(p, grid, stream));
+    HIP_TRY(hipEventRecord(ev1, stream));
+    std::vector<unsigned long long> res((r_bytes + 7) / 8);
+    int32_t ab = 0;
+    HIP_TRY(hipMemcpyAsync(res.data(), d_wres.p, r_bytes, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(&ab, p.abort, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, ev0, ev1));
+    *ms += t;
+    const int32_t* st = (const int32_t*)(res.data() + 2 * nwd);
+    const int32_t* fs = st + nwd;
+    const unsigned long long* ss = (const unsigned long long*)(fs + nwd);
+    for (int i = 0; i < nwd; ++i) {
+      const int h = dense_wd[i];
+      const bool unfinished = st[i] != ST_VALID && st[i] != ST_INVALID;
+      status[h] = ab && unfinished ? ST_ABORTED : st[i], fail_step[h] = fs[i], explored[h] = res[i];
+    }
+    stats[1] += 1;
+    stats[2] += (double)ss[1];
+    stats[12] += nwd;
+    stats[13] += t;
+    stats[31] += nwd;
+    stats[32] += t;
+    stats[34] += nwd;  // (counter histories on closure tables)
+    stats[35] += t;
+    stats[37] += (double)ss[0];
+    for (int i = 0; i < nwd; ++i) stats[38] += (double)res[i];
+    stats[43] = std::max(stats[43], 1.0);
+    // algorithmic bytes as run_wide's: per step and live word its X, its pulls and its store
+    double alg = 0;
+    for (int i = 0; i < nwd; ++i) {
+      const std::vector<uint32_t>& ws = wide_streams[dense_wd[i]];
+      size_t q = 0;
+      for (int tt = 0; tt < nst[i] && q + 2 < ws.size(); ++tt) {
+        if (fs[i] >= 0 && tt > fs[i] + 1) break;
+        const int n = __builtin_popcountll(((uint64_t)ws[q] | ((uint64_t)ws[q + 1] << 31)) >> 6);
+        alg += std::ldexp(1.0, n) * (n / 2.0 + 2.0) * 8.0;
+        q += 3;
+        while (q < ws.size() && (ws[q] & DENSE_OPW)) ++q;
+      }
+    }
+    stats[33] += alg;
+    if (debug())
+      fprintf(stderr, "[lincheck] wide counters: %d histories (tables of 2^%d words in HBM), %.3f ms, steps=%llu "
+              "Fout=%llu; words visited %llu, stored nonzero %llu\n", nwd, std::max(0, lmax - 6), t, ss[1], ss[0],
+              ss[2], ss[3]);
+    ran = true;
+    return 0;
+  }
+
   int run_wide(float* ms, bool& ran) {
+    if (model == LC_MODEL_COUNTER) return run_wctr(ms, ran);
     const int nwd = (int)dense_wd.size();
     std::vector<int64_t> sbeg(nwd);
     std::vector<int32_t> nst(nwd);

@@ -17,6 +17,7 @@
 // Failure: each step ORs "some X was nonzero" (step t-1's post-return frontier held a config)
 // into `any` as an atomicMax of t + 1 before its last barrier; after it every workgroup reads
 // the same value, so all leave together (an empty frontier stays empty).
+#include "ctab.hpp"
 #include "dense.hpp"
 #include "dense_ops.hpp"
 #include "device_common.hpp"
@@ -709,6 +710,361 @@ __global__ void __launch_bounds__(256) wide_gather_kernel(WideDumpParams d, cons
     out[i] = HbmTab::ld(&d.tab[dump_index(hw[i], d, sBin, sOff)]);
 }
 
+
+// ---- counter histories on the HBM tables (r5): ctab.hip's
+// closure tables (one bit per mask, the value a function of the mask, consistency an EQ lookup:
+// CounterModel.step, counter.clj:100-127) past the tile teams' 24 slots, to WCTR_LMAX, on the
+// pipelined grid-wide schedule above. A word holds the 64 masks over slots 0..5; slots >= 6 are
+// its hi bits (H = L - 6 <= 32, so one ranked table with a 32-bit index, no slabs). Per step (decoded by one wave into
+// the LDS ring): the per-slot requirement relative to the config's low sum (cq), the 64-entry
+// EQ table over the low sums and five 64-entry tables of hi delta sums (6 hi slots each) and one of 4 (slots 36, 37).
+constexpr int32_t WC_UNC = 0x3fffffff;    // cq sentinel: the op steps from any config
+constexpr int32_t WC_NEVER = -0x3fffffff;  // ... from none
+constexpr int WC_LO = 6;
+constexpr int WC_SLOTS = 40;  // per-slot tables (slots 0..37, padded)
+
+struct WCStep {
+  uint64_t live, fresh, keep_lo;
+  int32_t j, jp, H, start, base;
+  int32_t req[WC_SLOTS];
+  int32_t cq[WC_SLOTS];
+  int8_t d[WC_SLOTS];
+  int16_t sh[5][64];  // hi slots 6 + 6g .. 11 + 6g by (w >> 6g) & 63
+  int16_t sh5[4];     // hi slots 36, 37 by w >> 30
+  uint64_t eq[64];    // EQ[v]: positions p (low masks) with S_lo(p) - lo_min = v
+};
+
+__device__ __forceinline__ uint64_t wc_keep6(int k) {
+  switch (k) {
+    case 0: return 0x5555555555555555ull;
+    case 1: return 0x3333333333333333ull;
+    case 2: return 0x0f0f0f0f0f0f0f0full;
+    case 3: return 0x00ff00ff00ff00ffull;
+    case 4: return 0x0000ffff0000ffffull;
+    default: return 0x00000000ffffffffull;
+  }
+}
+
+__device__ __forceinline__ uint64_t wc_gate(const WCStep& st, int32_t c, int s) {
+  if (c == WC_UNC) return ~0ull;
+  const uint32_t i = (uint32_t)(c - s);
+  return i < 64u ? st.eq[i] : 0ull;
+}
+
+// Step stream of a wide counter history (host-built, WideParams.stream):
+//   header words 0, 1, 2  live slots 0..30 | live slots 31..61 (bit k - 31) | j, bit 31 clear
+//   per invocation since the previous step, ctab.hpp's two words (bit 31 set):
+//     w0 = slot[0:8) | flags[8:16) | (uint8_t)delta[16:24)        flags: CT_UNC, CT_NEVER
+//     w1 = (req + CTAB_REQ_BIAS) & 0x3fffffff
+//   (at most WCTR_MAX_NINV invocations per step: the whole step in one 64-lane read)
+//   a 0 word after the last step
+__global__ void __launch_bounds__(WPWG, WP_MINW) wctr_pipe_kernel(WideParams p) {
+  __shared__ uint32_t sBin[WB * WB];
+  __shared__ uint32_t sLay[WIDE_LOW_BITS + 2];
+  __shared__ WCStep sRing[WRING];
+  __shared__ uint64_t sSeg[WRING + 1];
+  __shared__ uint32_t sOff[WH + 2];
+  __shared__ unsigned long long sRed;
+  __shared__ int sAbort;
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < WB * WB; i += WPWG) {
+    const int n = i / WB, k = i % WB;
+    uint64_t c = 0;
+    if (k <= n) {
+      c = 1;
+      for (int q = 1; q <= k; ++q) c = c * (uint64_t)(n - k + q) / (uint64_t)q;
+    }
+    sBin[i] = (uint32_t)c;
+  }
+  if (tid == 0) sAbort = 0;
+  __syncthreads();
+  if (tid <= WIDE_LOW_BITS + 1) {
+    uint32_t o = 0;
+    for (int r = 0; r < tid; ++r) o += sBin[DENSE_WORD_BITS * WB + r];
+    sLay[tid] = o;
+  }
+  const int Hm = 63 - __clzll((long long)p.tab_words);  // (tab_words = 2^Hm, Hm <= 32)
+  if (tid <= WH + 1) {
+    uint32_t o = 0;
+    for (int r = 0; r < tid && r <= Hm; ++r) o += sBin[Hm * WB + r];
+    sOff[tid] = o;
+  }
+  const int nb = (int)gridDim.x, bx = (int)blockIdx.x;
+  const int lb = (nb & 7) == 0 && LC_WIDE_XCD ? (bx & 7) * (nb >> 3) + (bx >> 3) : bx;
+  const int64_t gtid = (int64_t)lb * WPWG + tid, gstride = (int64_t)gridDim.x * WPWG;
+  unsigned long long st_fout = 0, st_steps = 0, st_wv = 0, st_wnz = 0;
+  for (int i = 0; i < p.n && !sAbort; ++i) {
+    const int ns = p.nsteps[i];
+    uint64_t* const T0 = p.tab;
+    uint64_t* const T1 = p.tab + p.tab_words;
+    auto tab = [&](int t) { return (t & 1) ? T1 : T0; };
+    uint32_t* const anyv = p.anyv + p.anyv_off[i];
+    // the initial config: nothing linearized (mask 0 = word 0, position 0), read by step 0
+    if (blockIdx.x == 0 && tid == 0) HbmTab::st(&T1[0], 1ull);
+    int64_t pos = p.sbeg[i];
+    auto decode = [&](int t) {  // (wave 0) ctab.hip's ct_decode with 64-bit live masks
+      if (tid >= 64) return;
+      WCStep* dst = &sRing[t % WRING];
+      const WCStep* prev = t > 0 ? &sRing[(t - 1) % WRING] : nullptr;
+      const uint32_t wd = p.stream[pos + lane];
+      const uint64_t live = (uint64_t)(uint32_t)__shfl((int)wd, 0, 64) |
+                            ((uint64_t)(uint32_t)__shfl((int)wd, 1, 64) << 31);
+      const int j = __shfl((int)wd, 2, 64);
+      const int nw = (int)__builtin_ctzll(~(__ballot(lane >= 3 && (wd & DENSE_OPW)) >> 3));
+      const int ninv = nw >> 1;
+      int32_t req = prev && lane < WC_SLOTS ? prev->req[lane] : WC_UNC;
+      int32_t d = prev && lane < WC_SLOTS ? (int32_t)prev->d[lane] : 0;
+      for (int k = 0; k < ninv; ++k) {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)wd, 3 + 2 * k);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)wd, 4 + 2 * k);
+        if (lane == (int)(a & 63u)) {
+          const uint32_t fl = (a >> 8) & 0xffu;
+          d = (int32_t)(int8_t)(uint8_t)((a >> 16) & 0xffu);
+          req = (fl & CT_UNC) ? WC_UNC : (fl & CT_NEVER) ? WC_NEVER : (int32_t)(b & 0x3fffffffu) - CTAB_REQ_BIAS;
+        }
+      }
+      const uint64_t plive = prev ? prev->live : 0ull;
+      const int pj = prev ? prev->j : -1;
+      const int32_t base = prev ? prev->base + (int32_t)prev->d[pj] : 0;
+      int32_t slo = 0, lo_min = 0;
+#pragma unroll
+      for (int k = 0; k < WC_LO; ++k) {
+        const int32_t dk = __builtin_amdgcn_readlane(d, k);
+        if ((lane >> k) & 1) slo += dk;
+        lo_min += dk < 0 ? dk : 0;
+      }
+      if (lane < WC_SLOTS) {
+        dst->req[lane] = req;
+        dst->d[lane] = (int8_t)d;
+        dst->cq[lane] = req == WC_UNC || req == WC_NEVER ? req : req - base - lo_min + (lane >= WC_LO ? d : 0);
+      }
+      dst->eq[lane] = 0;
+      // (one wave's LDS operations stay in order: the zeroing lands before the ORs)
+      __hip_atomic_fetch_or(&dst->eq[slo - lo_min], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int g = 0; g < 5; ++g) {
+        int32_t sm = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const int32_t dk = __builtin_amdgcn_readlane(d, WC_LO + 6 * g + k);
+          if ((lane >> k) & 1) sm += dk;
+        }
+        dst->sh[g][lane] = (int16_t)sm;
+      }
+      if (lane < 4) {
+        const int32_t d36 = __builtin_amdgcn_readlane(d, 36), d37 = __builtin_amdgcn_readlane(d, 37);
+        dst->sh5[lane] = (int16_t)((lane & 1 ? d36 : 0) + (lane & 2 ? d37 : 0));
+      }
+      if (lane == 0) {
+        const int L = live ? 64 - __clzll((long long)live) : 0;
+        const uint64_t fresh = prev ? live & ~(plive & ~(1ull << pj)) : live;
+        uint64_t kl = ~0ull;
+        for (int k = 0; k < WC_LO; ++k)
+          if (fresh & (1ull << k)) kl &= wc_keep6(k);
+        dst->live = live;
+        dst->fresh = fresh;
+        dst->keep_lo = kl;
+        dst->base = base;
+        dst->j = j;
+        dst->jp = pj;
+        dst->H = L > WC_LO ? L - WC_LO : 0;
+        dst->start = 1 << 30;
+      }
+      pos += 3 + nw;
+    };
+    if (ns > 0) decode(0);
+    __syncthreads();
+    if (ns > 0 && tid == 0) sRing[0].start = 0;
+    if (!wide_sync(p, &sAbort)) break;
+    unsigned long long expl = 0;
+    int fail_t = -1, t_dec = ns > 0 ? 1 : 0, t_run = t_dec, t_ret = 0;
+    for (int s = 0; t_ret < ns; ++s) {
+      while (t_ret < t_run) {  // retire the steps whose last layer ran before this super-layer
+        const WCStep& r = sRing[t_ret % WRING];
+        if (r.start + r.H >= s) break;
+        if (t_ret > 0 && !((ld_agent(&anyv[t_ret >> 5]) >> (t_ret & 31)) & 1u)) {
+          fail_t = t_ret - 1;
+          break;
+        }
+        ++t_ret;
+        ++st_steps;
+      }
+      if (fail_t >= 0 || t_ret >= ns) break;
+      if (tid <= WRING) {
+        uint64_t acc = 0;
+        for (int t = t_ret; t < t_run && t - t_ret < tid; ++t) {
+          const WCStep& r = sRing[t % WRING];
+          const int q = s - r.start;
+          if (q >= 0 && q <= r.H) acc += sBin[r.H * WB + q];
+        }
+        sSeg[tid] = acc;
+      }
+      __syncthreads();
+      const uint64_t total = sSeg[t_run - t_ret];
+      uint32_t anyseg = 0;
+      for (int64_t g = gtid; g < (int64_t)total; g += gstride) {
+        int si = 0;
+        while (si + 1 < t_run - t_ret && sSeg[si + 1] <= (uint64_t)g) ++si;
+        const int t = t_ret + si;
+        const WCStep& r = sRing[t % WRING];
+        const int H = r.H, q = s - r.start;
+        const int k = max(H < LC_WIDE_KLO ? H : LC_WIDE_KLO, H - WIDE_LOW_BITS), hb = H - k;
+        uint32_t gi = (uint32_t)((uint64_t)g - sSeg[si]);
+        int pp = q - k > 0 ? q - k : 0;
+        for (;; ++pp) {
+          const uint32_t blk = sBin[hb * WB + pp] * sBin[k * WB + (q - pp)];
+          if (gi < blk || pp >= hb || pp >= q) break;
+          gi -= blk;
+        }
+        const uint32_t nlo = sBin[k * WB + (q - pp)];
+        const uint32_t hi_i = gi / nlo, lo_i = gi - hi_i * nlo;
+        const uint32_t w = (hb ? (p.words[sLay[pp] + hi_i] << k) : 0u) | p.words[sLay[q - pp] + lo_i];
+        const uint64_t live = r.live;
+        if ((uint64_t)w & ~(live >> WC_LO)) continue;
+        const int j = r.j, jp = r.jp;
+        const int s_hi = (int)r.sh[0][w & 63u] + (int)r.sh[1][(w >> 6) & 63u] + (int)r.sh[2][(w >> 12) & 63u] +
+                         (int)r.sh[3][(w >> 18) & 63u] + (int)r.sh[4][(w >> 24) & 63u] + (int)r.sh5[w >> 30];
+        uint32_t T0w;
+        const uint32_t iw = sOff[q] + colex_rank(w, sBin, &T0w);
+        uint64_t X = 0;
+        if (!(w & (uint32_t)(r.fresh >> WC_LO))) {  // the previous step's table through its return jp
+          const uint64_t* Bp = tab(t - 1);
+          if (jp >= WC_LO) X = HbmTab::ld(&Bp[sOff[q + 1] + colex_rank(w | (1u << (jp - WC_LO)), sBin)]);
+          else if (jp >= 0) X = (HbmTab::ld(&Bp[iw]) & ~wc_keep6(jp)) >> (1 << jp);
+          else X = HbmTab::ld(&Bp[iw]);
+          X &= r.keep_lo;
+        }
+        uint64_t* const B = tab(t);
+        // the gated pulls over w's hi bits (only j's when w holds j), ranked as wide_pulls_ranked
+        const uint32_t jh = j >= WC_LO ? 1u << (j - WC_LO) : 0u;
+        const uint32_t m = (w & jh) ? jh : w;
+        uint32_t x = (w & jh) ? w & ((jh << 1) - 1u) : w;
+        const uint32_t off_dn = q > 0 ? sOff[q - 1] : 0u;
+        uint32_t P1 = 0, P0 = 0;
+        uint64_t R = 0;
+        for (int ii = 0; x; ii += 8) {
+          int bb[8];
+          uint32_t ix[8];
+          uint64_t v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            bb[u] = x ? __builtin_ctz(x) : -1;
+            x &= x - 1;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            ix[u] = 0xffffffffu;
+            if (bb[u] >= 0) {
+              const uint32_t c0 = sBin[bb[u] * WB + ii + u], c1 = sBin[bb[u] * WB + ii + u + 1];
+              P0 += c0;
+              if ((m >> bb[u]) & 1u) ix[u] = off_dn + P1 + (T0w - P0);
+              P1 += c1;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = ix[u] != 0xffffffffu ? HbmTab::ld(&B[ix[u]]) : 0ull;
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (ix[u] != 0xffffffffu) R |= v[u] & wc_gate(r, r.cq[WC_LO + bb[u]], s_hi);
+        }
+        if (!(w & jh)) {  // the in-word closure (gated transfers to a fixpoint), then j if low
+          const bool jhi = j >= WC_LO;
+          const uint64_t notj = jhi ? ~0ull : wc_keep6(j);
+          R &= notj;
+          const uint32_t lo = (uint32_t)live & 63u & ~(jhi ? 0u : 1u << j);
+          uint64_t G[WC_LO];
+#pragma unroll
+          for (int kk = 0; kk < WC_LO; ++kk)
+            G[kk] = ((live >> kk) & 1u) ? wc_gate(r, r.cq[kk], s_hi) & wc_keep6(kk) & notj : 0ull;
+          for (;;) {
+            const uint64_t R0 = R;
+#pragma unroll
+            for (int kk = 0; kk < WC_LO; ++kk)
+              if ((lo >> kk) & 1u) R |= ((X | R) & G[kk]) << (1 << kk);
+            if (R == R0) break;
+          }
+          if (!jhi) {
+#pragma unroll
+            for (int kk = 0; kk < WC_LO; ++kk)
+              if (kk == j) R |= ((X | R) & G[kk]) << (1 << kk);
+          }
+        }
+        HbmTab::st(&B[iw], X | R);
+        expl += (uint64_t)__popcll(R);
+        if (t > 0) st_fout += (uint64_t)__popcll(X);
+        if (X) anyseg |= 1u << si;
+        ++st_wv, st_wnz += (X | R) != 0;
+      }
+      for (int si = 0; si < t_run - t_ret; ++si)
+        if (__any((anyseg >> si) & 1u) && lane == 0) {
+          const int t = t_ret + si;
+          __hip_atomic_fetch_or(&anyv[t >> 5], 1u << (t & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      const int t_dec_old = t_dec;
+      if (t_dec < ns && t_dec - t_ret < WRING - 1) {
+        decode(t_dec);
+        ++t_dec;
+      }
+      __syncthreads();
+      if (t_run < t_dec_old) {
+        bool ok = true;
+        if (t_run - 1 >= t_ret) {
+          const WCStep& pr = sRing[(t_run - 1) % WRING];
+          const int gap = pr.j < WC_LO ? 1 : 2;
+          ok = s + 1 - pr.start >= min(gap, pr.H + 1);
+        }
+        if (ok) {
+          if (tid == 0) sRing[t_run % WRING].start = s + 1;
+          ++t_run;
+        }
+      }
+      if (!wide_sync(p, &sAbort)) break;
+    }
+    if (sAbort) break;
+    if (fail_t < 0 && ns > 0) {  // the last step's return: its frontier must hold a config
+      const WCStep& r = sRing[(ns - 1) % WRING];
+      const int pj = r.j;
+      const uint64_t lv = r.live & ~(1ull << pj);
+      const int Lf = lv ? 64 - __clzll((long long)lv) : 0;
+      const int64_t nwt = (int64_t)1 << (Lf > WC_LO ? Lf - WC_LO : 0);
+      const uint64_t* const Bl = tab(ns - 1);
+      uint64_t nz = 0;
+      for (int64_t w = gtid; w < nwt; w += gstride) {
+        if ((uint64_t)w & ~(lv >> WC_LO)) continue;
+        const uint32_t wr = pj >= WC_LO ? (uint32_t)w | (1u << (pj - WC_LO)) : (uint32_t)w;
+        uint64_t X = HbmTab::ld(&Bl[sOff[__popc(wr)] + colex_rank(wr, sBin)]);
+        if (pj < WC_LO) X = (X & ~wc_keep6(pj)) >> (1 << pj);
+        st_fout += (uint64_t)__popcll(X);
+        nz |= X;
+      }
+      if (__any(nz != 0) && lane == 0)
+        __hip_atomic_fetch_or(&anyv[ns >> 5], 1u << (ns & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!wide_sync(p, &sAbort)) break;
+      if (!((ld_agent(&anyv[ns >> 5]) >> (ns & 31)) & 1u)) fail_t = ns - 1;
+    }
+    for (int off = 32; off > 0; off >>= 1) expl += __shfl_down(expl, off, 64);
+    if (tid == 0) sRed = 0;
+    __syncthreads();
+    if (lane == 0 && expl) atomicAdd(&sRed, expl);
+    __syncthreads();
+    if (tid == 0 && sRed) atomicAdd(&p.explored[i], sRed);
+    if (!wide_sync(p, &sAbort)) break;
+    if (blockIdx.x == 0 && tid == 0) {
+      p.status[i] = fail_t >= 0 ? ST_INVALID : ST_VALID;
+      p.fail_step[i] = fail_t;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    st_fout += __shfl_down(st_fout, off, 64);
+    st_wv += __shfl_down(st_wv, off, 64);
+    st_wnz += __shfl_down(st_wnz, off, 64);
+  }
+  if (lane == 0 && st_fout) atomicAdd(&p.stats[0], st_fout);
+  if (blockIdx.x == 0 && tid == 0 && st_steps) atomicAdd(&p.stats[1], st_steps);
+  if (lane == 0 && st_wv) atomicAdd(&p.stats[2], st_wv);
+  if (lane == 0 && st_wnz) atomicAdd(&p.stats[3], st_wnz);
+}
+
 }  // namespace
 
 int wide_grid_size(bool pipe) {
@@ -738,6 +1094,24 @@ hipError_t launch_wide_gather(const WideDumpParams& d, const uint64_t* hw, uint6
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(wide_gather_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, d, hw, out, n);
   return hipGetLastError();
+}
+
+int wctr_grid_size() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)wctr_pipe_kernel, WPWG, 0) != hipSuccess ||
+      per_cu < 1)
+    return 0;
+  return prop.multiProcessorCount * per_cu;
+}
+
+hipError_t launch_wctr(const WideParams& p, int grid, hipStream_t stream) {
+  WideParams q = p;
+  void* args[] = {&q};
+  return hipLaunchCooperativeKernel((const void*)wctr_pipe_kernel, dim3(grid), dim3(WPWG), args, 0, stream);
 }
 
 hipError_t launch_wide(const WideParams& p, int grid, hipStream_t stream) {

@@ -80,6 +80,12 @@ hipError_t launch_wide_dump(const WideDumpParams& d, hipStream_t stream);
 // out[i] = the word of tab (as d: layout, Hm) at hi-bit word hw[i]
 hipError_t launch_wide_gather(const WideDumpParams& d, const uint64_t* hw, uint64_t* out, int n, hipStream_t stream);
 int wide_grid_size(bool pipe);
+// counter histories on the HBM tables (wctr_pipe_kernel): live width up to
+// WCTR_LMAX, the stream in wide.hip's counter format, tab_words = 2^(lmax - 6)
+constexpr int WCTR_LMAX = 38;      // 2 tables of 2^32 words (64 GiB): the word index stays 32-bit
+constexpr int WCTR_MAX_NINV = 30;  // invocations per step (3 header words + 2 per invocation in 64 lanes)
+hipError_t launch_wctr(const WideParams& p, int grid, hipStream_t stream);
+int wctr_grid_size();
 size_t wide_bar_bytes();
 
 }  // namespace lc

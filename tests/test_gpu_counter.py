@@ -233,3 +233,88 @@ def test_gpu_ctab_teams_past_20_slots_vs_oracle():
     for k in range(h.n_hist):
         _cmp(g, exp[k], k, f"counter width {widths[k]}")
     assert any(e["valid"] == 0 for e in exp) and any(e["valid"] == 1 for e in exp)
+
+
+# ---- counters on the HBM tables (wctr_pipe_kernel): live width 25..36 --------
+
+@pytest.mark.parametrize("grid", ["0", "8"])
+def test_gpu_wctr_vs_oracle(grid, monkeypatch):
+    """the counter closure tables in HBM (one ranked table of 2^(L-6) words,
+    the grid-wide pipelined schedule of wide.hip, ctab's EQ gates), with LC_WCTR_MINW=1 routing
+    every counter to them (in production they take widths 25..36 only): random histories with
+    crashed ops, :fail reads and perturbed reads, bit-exact with the oracle (verdict, failing
+    :index triple, explored). LC_WIDE_GRID=8 runs the grid on 8 workgroups."""
+    monkeypatch.setenv("LC_WCTR_MINW", "1")
+    monkeypatch.setenv("LC_WIDE_GRID", grid)
+    h = _mixed_counters(80, 7300 + int(grid), max_ops=250, max_clients=16, max_crash=4)
+    g = _lib.check(2, 0, h)
+    st = _lib.check_stats()
+    assert int(st["wide_histories"]) == h.n_hist, st
+    exp = oracle.check_many("counter", h, n_threads=8)
+    for k in range(h.n_hist):
+        _cmp(g, exp[k], k, f"wctr grid={grid}")
+    assert any(e["valid"] == 0 for e in exp) and any(e["valid"] == 1 for e in exp)
+
+
+@pytest.mark.parametrize("init", [0, -123456])
+def test_gpu_wctr_matches_ctab(init, monkeypatch):
+    """The same counters on the HBM tables (LC_WCTR_MINW=1) and on the LDS tables / tile teams."""
+    h = H.concat([synth.gen_counter(400, 16, 0.0, 7400 + t, n_crashed=t % 5, invalid=(t % 3 == 1)) for t in range(12)])
+    a = _lib.check(2, init, h)
+    assert int(_lib.check_stats()["wide_histories"]) == 0
+    monkeypatch.setenv("LC_WCTR_MINW", "1")
+    b = _lib.check(2, init, h)
+    assert int(_lib.check_stats()["wide_histories"]) == h.n_hist
+    for key in ("valid", "fail_idx", "fail_inv", "prev_ok", "explored", "err"):
+        assert np.array_equal(a[key], b[key]), key
+
+
+def test_gpu_wctr_counter_ramp_vs_oracle():
+    """The counter crash ramp past the tile teams (K = 10, 12, 14: live width 25, 27, 29; the
+    grid kernel's range until r5) on the HBM tables, against the oracle's explored counts and
+    verdicts (tests/golden/counter_ramp_oracle.json, from tools/crash_ramp.py --model counter)."""
+    fx = json.load(open(os.path.join(GOLD_DIR, "counter_ramp_oracle.json")))
+    cases = {c["crashed"]: c for c in fx["cases"]}
+    for k in (10, 12, 14):
+        h = synth.gen_counter(2000, 16, 0.0, 0x5EED4000 + 0x100 + k, n_crashed=k, crash_span=0.2)
+        assert _live_width(h, 0) == cases[k]["width"]
+        g = _lib.check(2, 0, h)
+        st = _lib.check_stats()
+        assert int(st["wide_histories"]) == 1, (k, st)
+        assert (int(g["valid"][0]), int(g["explored"][0])) == (cases[k]["valid"], cases[k]["explored"]), k
+
+
+def test_gpu_wctr_widths_36_38_vs_oracle():
+    """The widest counter tables (36 and 38 live slots; 2 x 2^32 words at 38): a 40-op base with up to 32 calls that
+    are pending throughout and can never apply (add-and-get [1 10^9], completed :info at the end:
+    a vector value is checked even for :info, counter.clj:114-119, and no config reaches 10^9 - 1),
+    valid and invalid, against the oracle; the explored count is the base's."""
+    for bad, seed, width in ((False, 7500, 36), (True, 7501, 36), (False, 7502, 38), (True, 7503, 38)):
+        base = synth.gen_counter(40, 6, 0.0, seed, invalid=bad)
+        n = width - _live_width(base, 0)
+        # the never-ops invoked in two groups around the base's first completion (a step holds at
+        # most WCTR_MAX_NINV = 30 invocations), completed :info at the end
+        c0 = int(np.nonzero(np.asarray(base.type) != 0)[0][0]) + 1
+        half = n // 2
+        seg = lambda a, b: np.arange(a, b)  # noqa: E731
+        rows = [("x", seg(0, half)), ("b", seg(0, c0)), ("x", seg(half, n)), ("b", seg(c0, int(base.n))), ("y", seg(0, n))]
+        cols = {k: [] for k in ("proc", "typ", "f", "v0", "v1", "vf")}
+        for kind, ix in rows:
+            if kind == "b":
+                vals = (base.process[ix], base.type[ix], base.f[ix], base.v0[ix], base.v1[ix], base.vflags[ix])
+            else:  # add-and-get [1 10^9]: invoked ("x"), completed :info ("y")
+                vals = (20000 + ix, np.full(len(ix), 0 if kind == "x" else 3), np.full(len(ix), 5),
+                        np.full(len(ix), 1), np.full(len(ix), 10 ** 9), np.full(len(ix), H.V_PAIR))
+            for key, v in zip(cols, vals):
+                cols[key].append(np.asarray(v))
+        c = {k: np.concatenate(v) for k, v in cols.items()}
+        h = H.from_columns(np.arange(len(c["proc"])), c["proc"].astype(np.int32), c["typ"].astype(np.int8),
+                           c["f"].astype(np.int8), c["v0"].astype(np.int64), c["v1"].astype(np.int64),
+                           c["vf"].astype(np.int8))
+        w = _live_width(h, 0)
+        assert w == width, w
+        g = _lib.check(2, 0, h)
+        assert int(_lib.check_stats()["wide_histories"]) == 1
+        e = oracle.check_one("counter", h)
+        _cmp(g, e, 0, f"wctr w={w} bad={bad}")
+        assert int(g["explored"][0]) == oracle.check_one("counter", base)["explored"]
