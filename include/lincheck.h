@@ -39,7 +39,8 @@ extern "C" {
                             4: LC_H_ABORTED, statistics 34..38 (counter closure tables);
                             5: statistic 42 (counter tile teams), failure configs of histories
                                on the HBM tables (no LC_E_CONFIGS for their width);
-                            6: HBM tables to live width 36 in slabs, statistic 43 */
+                            6: HBM tables to live width 36 in slabs, statistic 43; counters
+                               on HBM tables (widths 25..38) */
 
 enum lc_model { LC_MODEL_CAS_REGISTER = 1, LC_MODEL_COUNTER = 2, LC_MODEL_LEADER = 3 };
 enum lc_valid { LC_INVALID = 0, LC_VALID = 1, LC_UNKNOWN = 2 };
@@ -220,7 +221,8 @@ int32_t lc_plan_results(lc_plan* p, int8_t* out_valid, int64_t* out_fail_idx,
  *    hipSetDevice, 22 streams/events/occupancy queries, 23 uploads, 24 dense step streams
  * 25..27 dense big kernel: frontier configs in, frontier configs out, configs explored
  * 28..30 the same for the dense wave (+ MID) kernel
- * 31 histories decided on closure tables in HBM (wide.hip: live width 25..36; counted in 12 too)
+ * 31 histories decided on closure tables in HBM (wide.hip: cas-register live width 25..36, counters
+ *    25..38; counted in 12 too, counters in 34 too)
  * 32 their kernel's ms (part of 0 and 13)
  * 33 their algorithmic HBM bytes: per step and live word, its X, its pulls and its store (8 B each)
  * 34 counter histories decided on closure tables (ctab.hip; counted in 12 too)  35 their kernel's ms
