@@ -15,8 +15,13 @@ h = synth.gen_config("c3")
 w = [C.live_width(h, k) for k in range(h.n_hist)]
 one = h.select([258])
 wide = h.select([k for k in range(h.n_hist) if w[k] >= 17])
+# argv: the runs (alone258, teams) and the tile sizes, e.g. alone258 plan,14,13,12
+runs = sys.argv[1].split("+") if len(sys.argv) > 1 else ["alone258", "teams"]
+lbs = [x if x != "plan" else "" for x in sys.argv[2].split("+")] if len(sys.argv) > 2 else ["", "17", "16", "15", "14"]
 for name, hh in (("alone258", one), ("teams", wide)):
-    for lb in ("", "17", "16", "15", "14"):
+    if name not in runs:
+        continue
+    for lb in lbs:
         if lb:
             os.environ["LC_TILE_LBITS"] = lb
         elif "LC_TILE_LBITS" in os.environ:
