@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -2039,6 +2040,156 @@ struct lc_plan {
     uint64_t mask;
     int state, last_step;  // state id (0 = nil); the step whose closure produced it (-1: initial)
   };
+  // Failure report of a counter history on the HBM tables (wctr_pipe_kernel), as wide_report:
+  // the run stopped before the failing RETURN t, step t - 1's table dumped through its returning
+  // slot (wctr_dump_kernel: masks), each config's :last-op walked back. At step s a config of
+  // mask m (without j_s) was produced by linearizing j_s last iff m is in step s's table and j_s's
+  // requirement holds at m (CounterModel.step, counter.clj:102-127: S(m) = req - base, or j_s
+  // unconstrained); else it was carried and held j_s already (m | j_s one step earlier).
+  // out: (mask, value = init + base + S(mask), producing step) per config.
+  struct CtrCfg {
+    uint64_t mask;
+    int64_t value;
+    int last_step;
+  };
+  int wctr_report(int t_fail, std::vector<CtrCfg>& out) {
+    out.clear();
+    const int64_t init = enc.init_value;
+    if (t_fail <= 0) {
+      out.push_back({0ull, init, -1});
+      return 0;
+    }
+    // per step (the decoder's state): live slots, j, base, j's delta / requirement / flags, and
+    // the slot deltas (for the sums of the walk and the values)
+    const std::vector<uint32_t>& ws = wide_streams[0];
+    std::vector<uint64_t> live_s;
+    std::vector<int> j_s;
+    std::vector<int64_t> base_s;
+    std::vector<std::array<int8_t, 64>> d_s;
+    std::vector<int32_t> req_s;
+    std::vector<uint32_t> fl_s;
+    {
+      std::array<int8_t, 64> d{};
+      int32_t req[64] = {0};
+      uint32_t fl[64];
+      for (int k = 0; k < 64; ++k) fl[k] = CT_UNC;
+      int64_t base = 0;
+      size_t q = 0;
+      while (q + 2 < ws.size() && (int)live_s.size() < t_fail) {
+        if (!j_s.empty()) base += d_s.back()[j_s.back()];
+        const uint64_t live = (uint64_t)ws[q] | ((uint64_t)ws[q + 1] << 31);
+        const int j = (int)ws[q + 2];
+        q += 3;
+        for (; q + 1 < ws.size() && (ws[q] & DENSE_OPW); q += 2) {
+          const uint32_t a = ws[q], b = ws[q + 1], sl = a & 63u;
+          fl[sl] = (a >> 8) & 0xffu;
+          d[sl] = (int8_t)(uint8_t)((a >> 16) & 0xffu);
+          req[sl] = (int32_t)(b & 0x3fffffffu) - CTAB_REQ_BIAS;
+        }
+        live_s.push_back(live), j_s.push_back(j), base_s.push_back(base), d_s.push_back(d);
+        req_s.push_back(req[j]), fl_s.push_back(fl[j]);
+      }
+      if ((int)live_s.size() < t_fail) {
+        last_error = "failure configs: the wide counter stream ends before the failing step";
+        return LC_E_INTERNAL;
+      }
+    }
+    auto sum_of = [&](uint64_t m, int s) {
+      int64_t v = 0;
+      for (; m; m &= m - 1) v += d_s[s][__builtin_ctzll(m)];
+      return v;
+    };
+    auto run_to = [&](int stop) -> int {
+      wide_stop = stop;
+      wide_ran = false;
+      const int rc = run();
+      wide_stop = -1;
+      if (rc) return rc;
+      if (!wide_ran) {
+        last_error = "failure configs: the history did not run on the HBM tables";
+        return LC_E_CONFIGS;
+      }
+      return 0;
+    };
+    int rc = run_to(t_fail);
+    if (rc) return rc;
+    const int64_t tw = (int64_t)1 << wide_last_hm;
+    auto table_of = [&](int s) { return d_wtab.as<uint64_t>() + ((s & 1) ? tw : 0); };
+    WideDumpParams dp{};
+    dp.ranked = 1;
+    dp.Hm = wide_last_hm;
+    dp.split = 0;
+    const int64_t cap = (int64_t)1 << 22;
+    DevArray d_masks, d_cnt;
+    HIP_TRY(d_masks.ensure((size_t)cap * 8));
+    HIP_TRY(d_cnt.ensure(8));
+    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 8, stream));
+    dp.tab = table_of(t_fail - 1);
+    dp.jp = j_s[t_fail - 1];
+    dp.lv = live_s[t_fail - 1] & ~(1ull << dp.jp);
+    dp.cap = cap;
+    dp.masks = d_masks.as<uint64_t>();
+    dp.count = d_cnt.as<unsigned long long>();
+    HIP_TRY(launch_wctr_dump(dp, stream));
+    unsigned long long cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, d_cnt.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if ((int64_t)cnt > cap) {
+      last_error = "failure configs unavailable: the pre-failure frontier holds " + std::to_string(cnt) +
+                   " configs, more than the dump's " + std::to_string(cap);
+      return LC_E_CONFIGS;
+    }
+    std::vector<uint64_t> masks(cnt);
+    HIP_TRY(hipMemcpy(masks.data(), d_masks.p, cnt * 8, hipMemcpyDeviceToHost));
+    // the value: the ops returned before step t_fail plus the mask's (slot deltas as of step
+    // t_fail - 1: a slot invoked at t_fail is fresh, never in the mask)
+    const int64_t base_f = base_s[t_fail - 1] + d_s[t_fail - 1][j_s[t_fail - 1]];
+    out.resize(cnt);
+    std::vector<uint64_t> cur(cnt);
+    std::vector<int> open;
+    for (size_t i = 0; i < cnt; ++i) {
+      out[i] = {masks[i], init + base_f + sum_of(masks[i], t_fail - 1), -2};
+      cur[i] = masks[i];
+      open.push_back((int)i);
+    }
+    int S = t_fail;
+    DevArray d_hw, d_words;
+    std::vector<uint64_t> hw, words;
+    for (int st = t_fail - 1; st >= 0 && !open.empty(); --st) {
+      if (st < S - 2) {
+        S = st + 1;
+        if ((rc = run_to(S))) return rc;
+      }
+      hw.resize(open.size());
+      for (size_t k = 0; k < open.size(); ++k) hw[k] = cur[open[k]] >> 6;
+      HIP_TRY(d_hw.ensure(hw.size() * 8));
+      HIP_TRY(d_words.ensure(hw.size() * 8));
+      HIP_TRY(hipMemcpy(d_hw.p, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
+      dp.tab = table_of(st);
+      HIP_TRY(launch_wide_gather(dp, d_hw.as<uint64_t>(), d_words.as<uint64_t>(), (int)hw.size(), stream));
+      words.resize(hw.size());
+      HIP_TRY(hipMemcpyAsync(words.data(), d_words.p, words.size() * 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      const int j = j_s[st];
+      std::vector<int> still;
+      for (size_t k = 0; k < open.size(); ++k) {
+        const int i = open[k];
+        const bool in_tab = (words[k] >> (cur[i] & 63u)) & 1u;
+        bool produced = in_tab;
+        if (produced && !(fl_s[st] & CT_UNC))
+          produced = !(fl_s[st] & CT_NEVER) && sum_of(cur[i], st) == (int64_t)req_s[st] - base_s[st];
+        if (produced) out[i].last_step = st;
+        else cur[i] |= 1ull << j, still.push_back(i);
+      }
+      open.swap(still);
+    }
+    if (!open.empty()) {
+      last_error = "failure configs: a config's :last-op walk reached the history's start";
+      return LC_E_CONFIGS;
+    }
+    return 0;
+  }
+
   int wide_report(int t_fail, std::vector<RepCfg>& out) {
     out.clear();
     if (t_fail <= 0) {  // the failing RETURN is the first: its frontier is the initial config
@@ -2195,7 +2346,7 @@ struct lc_plan {
     for (int i = 0; i < nwd; ++i) {
       const int h = dense_wd[i];
       sbeg[i] = (int64_t)words.size();
-      nst[i] = enc.n_steps(h);
+      nst[i] = wide_stop >= 0 ? std::min(enc.n_steps(h), wide_stop) : enc.n_steps(h);
       lmx[i] = (int8_t)enc.live_max[h];
       lmax = std::max(lmax, (int)enc.live_max[h]);
       words.insert(words.end(), wide_streams[h].begin(), wide_streams[h].end());
@@ -2286,6 +2437,8 @@ struct lc_plan {
     stats[37] += (double)ss[0];
     for (int i = 0; i < nwd; ++i) stats[38] += (double)res[i];
     stats[43] = std::max(stats[43], 1.0);
+    wide_last_ranked = true, wide_last_hm = std::max(0, lmax - 6), wide_last_split = 0;
+    wide_ran = true;
     // algorithmic bytes as run_wide's: per step and live word its X, its pulls and its store
     double alg = 0;
     for (int i = 0; i < nwd; ++i) {
@@ -3143,6 +3296,41 @@ int32_t lc_failure_configs(int32_t hist, int32_t k, int64_t* state, int8_t* is_n
       return rc;
     }
     return emit(all, WIDE_LMAX);
+  }
+  // a counter decided on the HBM counter tables (wctr_pipe_kernel): the same, from those tables
+  if (p->enc.model == LC_MODEL_COUNTER && !p->dense_wd.empty() &&
+      !(getenv("LC_WIDE_CONFIGS") && atoi(getenv("LC_WIDE_CONFIGS")) == 0)) {
+    std::vector<lc_plan::CtrCfg> all;
+    rc = p->wctr_report(t_fail, all);
+    if (rc) {
+      set_err(err, err_len, "%s", p->last_error.c_str());
+      return rc;
+    }
+    std::sort(all.begin(), all.end(), [](const lc_plan::CtrCfg& x, const lc_plan::CtrCfg& y) { return x.mask < y.mask; });
+    {
+      std::vector<lc_plan::RepCfg> none;
+      emit(none, 0);  // the pending ops and an empty output, then the configs below
+    }
+    int64_t newest = -1;
+    for (const auto& c : all) newest = std::max(newest, last_of_step(c.last_step));
+    if (out_last_op) *out_last_op = newest;
+    int out = 0;
+    for (const auto& c : all) {
+      if (out >= k) break;
+      int nl = 0;
+      for (int s = 0; s < 64; ++s)
+        if ((c.mask >> s) & 1) {
+          if (linearized) linearized[(size_t)out * 64 + nl] = slot_inv[s];
+          ++nl;
+        }
+      if (state) state[out] = c.value;
+      if (is_nil) is_nil[out] = 0;
+      if (n_lin) n_lin[out] = nl;
+      if (last_op) last_op[out] = last_of_step(c.last_step);
+      ++out;
+    }
+    if (n_out) *n_out = out;
+    return 0;
   }
   // stop before the failing RETURN: the frontier it saw stays in flist (the grid kernel: the
   // dense tables keep no config lists), each config tagged with the step that emitted it. A key

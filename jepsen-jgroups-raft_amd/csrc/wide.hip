@@ -1065,6 +1065,43 @@ __global__ void __launch_bounds__(WPWG, WP_MINW) wctr_pipe_kernel(WideParams p) 
   if (lane == 0 && st_wnz) atomicAdd(&p.stats[3], st_wnz);
 }
 
+// failure reports of counter histories on the HBM tables: as wide_dump_kernel, configs are masks
+// (the value is a function of the mask): tab = step t - 1's table (ranked over Hm hi bits, 64
+// masks per word), read through its returning slot jp, over the post-return live slots lv
+__global__ void __launch_bounds__(256) wctr_dump_kernel(WideDumpParams d) {
+  __shared__ uint32_t sBin[WB * WB];
+  __shared__ uint32_t sOff[WH + 2];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < WB * WB; i += 256) {
+    const int n = i / WB, k = i % WB;
+    uint64_t c = 0;
+    if (k <= n) {
+      c = 1;
+      for (int q = 1; q <= k; ++q) c = c * (uint64_t)(n - k + q) / (uint64_t)q;
+    }
+    sBin[i] = (uint32_t)c;
+  }
+  __syncthreads();
+  if (tid <= WH + 1) {
+    uint32_t o = 0;
+    for (int r = 0; r < tid && r <= d.Hm; ++r) o += sBin[d.Hm * WB + r];
+    sOff[tid] = o;
+  }
+  __syncthreads();
+  const int Lf = d.lv ? 64 - __clzll((long long)d.lv) : 0;
+  const int64_t nwt = (int64_t)1 << (Lf > WC_LO ? Lf - WC_LO : 0);
+  for (int64_t w = (int64_t)blockIdx.x * 256 + tid; w < nwt; w += (int64_t)gridDim.x * 256) {
+    if ((uint64_t)w & ~(d.lv >> WC_LO)) continue;
+    const uint32_t wr = d.jp >= WC_LO ? (uint32_t)w | (1u << (d.jp - WC_LO)) : (uint32_t)w;
+    uint64_t X = HbmTab::ld(&d.tab[sOff[__popc(wr)] + colex_rank(wr, sBin)]);
+    if (d.jp < WC_LO) X = (X & ~wc_keep6(d.jp)) >> (1 << d.jp);
+    if (!X) continue;
+    unsigned long long at = atomicAdd(d.count, (unsigned long long)__popcll(X));
+    for (; X; X &= X - 1, ++at)
+      if ((int64_t)at < d.cap) d.masks[at] = ((uint64_t)w << WC_LO) | (uint64_t)__builtin_ctzll(X);
+  }
+}
+
 }  // namespace
 
 int wide_grid_size(bool pipe) {
@@ -1106,6 +1143,11 @@ int wctr_grid_size() {
       per_cu < 1)
     return 0;
   return prop.multiProcessorCount * per_cu;
+}
+
+hipError_t launch_wctr_dump(const WideDumpParams& d, hipStream_t stream) {
+  hipLaunchKernelGGL(wctr_dump_kernel, dim3(1024), dim3(256), 0, stream, d);
+  return hipGetLastError();
 }
 
 hipError_t launch_wctr(const WideParams& p, int grid, hipStream_t stream) {

@@ -85,6 +85,8 @@ int wide_grid_size(bool pipe);
 constexpr int WCTR_LMAX = 38;      // 2 tables of 2^32 words (64 GiB): the word index stays 32-bit
 constexpr int WCTR_MAX_NINV = 30;  // invocations per step (3 header words + 2 per invocation in 64 lanes)
 hipError_t launch_wctr(const WideParams& p, int grid, hipStream_t stream);
+// failure reports: the configs (masks) of tab (ranked over Hm hi bits, 64 masks per word) through jp
+hipError_t launch_wctr_dump(const WideDumpParams& d, hipStream_t stream);
 int wctr_grid_size();
 size_t wide_bar_bytes();
 

@@ -318,3 +318,44 @@ def test_gpu_wctr_widths_36_38_vs_oracle():
         e = oracle.check_one("counter", h)
         _cmp(g, e, 0, f"wctr w={w} bad={bad}")
         assert int(g["explored"][0]) == oracle.check_one("counter", base)["explored"]
+        if bad:  # the failure report from the width-36/38 tables
+            _configs_vs_oracle(h, f"wctr w={w}")
+
+
+def _configs_vs_oracle(h, what):
+    e = oracle.check_one("counter", h, with_configs=True)
+    assert e["valid"] == 0, what
+    cfgs, pending, lasts, newest = _lib.failure_configs(0, 1 << 12, with_last=True)
+    assert sorted(pending) == sorted(e["pending_inv_idx"]), what
+    assert set(cfgs) == e["fail_configs"] and len(cfgs) == len(e["fail_configs"]), what
+    for c, last in zip(cfgs, lasts):
+        assert last == e["fail_last_op"][c], (what, c, last, e["fail_last_op"][c])
+    assert newest == max(e["fail_last_op"].values()), what
+    return sum(1 for x in lasts if x != e["prev_ok_idx"])
+
+
+def test_gpu_wctr_failure_configs_match_oracle(monkeypatch):
+    """Failure reports straight from the HBM counter tables (a re-run stopped before the failing
+    RETURN, the frontier dumped as masks, each config's :last-op walked back with the counter's
+    gate): every counter forced onto them (LC_WCTR_MINW=1), against the oracle as sets with the
+    per-config :last-op and the newest, and against the grid kernel's report (LC_WIDE_CONFIGS=0)."""
+    monkeypatch.setenv("LC_WCTR_MINW", "1")
+    found = carried = 0
+    for t in range(30):
+        h = synth.gen_counter(80, 4, 0.1, 9000 + t, invalid=True, n_crashed=t % 3)
+        g = _lib.check(2, 0, h)
+        assert int(_lib.check_stats()["wide_histories"]) == 1
+        e = oracle.check_one("counter", h)
+        assert int(g["valid"][0]) == e["valid"]
+        if e["valid"] != 0:
+            continue
+        carried += _configs_vs_oracle(h, f"t={t}")
+        found += 1
+        if t % 5 == 0:
+            a = _lib.failure_configs(0, 1 << 12, with_last=True)
+            monkeypatch.setenv("LC_WIDE_CONFIGS", "0")
+            b = _lib.failure_configs(0, 1 << 12, with_last=True)
+            monkeypatch.delenv("LC_WIDE_CONFIGS")
+            assert sorted(zip(a[0], a[2])) == sorted(zip(b[0], b[2])), t  # (configs with their :last-op)
+            assert sorted(a[1]) == sorted(b[1]) and a[3] == b[3], t
+    assert found > 5 and carried > 0
