@@ -9,6 +9,9 @@ These fixtures are the oracle's answers on:
               runs on the HBM tables
   ramp14      K = 14 (width 27, ~17 G configs)
   ramp16      K = 16 (width 30, ~59 G configs; hours, and only if its frontier fits memory)
+  ramp11s     r5: a 1,000-op ramp history, 16 clients, K = 11: live width 25 (HBM tables)
+  ramp10c17   r5: 1,000 ops, 17 clients, K = 10: width 25
+  ramp11c17   r5: 1,000 ops, 17 clients, K = 11: width 26
   ramp13x50   ramp13 with one :ok read perturbed at 50 % of the history: the pipelined HBM-table
               kernel must stop mid-history with later steps already in flight
   c4x15       C4 (100k ops, width 23: the rotated 128-tile team) with one read perturbed at 15 %
@@ -52,6 +55,14 @@ GEN = {
                lambda: ramp(14)),
     "ramp16": ("cas-register", "synth.gen_register(2000, 16, 0.002, 0x5EED4000 + 16, n_crashed=16)",
                lambda: ramp(16)),
+    # r5: real wide frontiers the oracle can finish in the build container (the K = 13 history
+    # needs > 36 GB: OOM-killed here): 1,000-op ramp histories just past the tile teams
+    "ramp11s": ("cas-register", "synth.gen_register(1000, 16, 0.002, 0x5EED4000 + 11, n_crashed=11)",
+                lambda: synth.gen_register(1000, 16, 0.002, RAMP_SEED0 + 11, n_crashed=11)),
+    "ramp10c17": ("cas-register", "synth.gen_register(1000, 17, 0.002, 0x5EED4000 + 10, n_crashed=10)",
+                  lambda: synth.gen_register(1000, 17, 0.002, RAMP_SEED0 + 10, n_crashed=10)),
+    "ramp11c17": ("cas-register", "synth.gen_register(1000, 17, 0.002, 0x5EED4000 + 11, n_crashed=11)",
+                  lambda: synth.gen_register(1000, 17, 0.002, RAMP_SEED0 + 11, n_crashed=11)),
     "ramp13x50": ("cas-register",
                   "synth.perturb_read(synth.gen_register(2000, 16, 0.002, 0x5EED4000 + 13, "
                   "n_crashed=13), 0.5, 'cas-register', 50)",
