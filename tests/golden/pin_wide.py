@@ -15,6 +15,10 @@ These fixtures are the oracle's answers on:
   ramp13x50   ramp13 with one :ok read perturbed at 50 % of the history: the pipelined HBM-table
               kernel must stop mid-history with later steps already in flight
   c4x15       C4 (100k ops, width 23: the rotated 128-tile team) with one read perturbed at 15 %
+              (r5: the changed value stays explainable, so the history is still valid: a second
+              full-size C4 count, 10,994,825,722 configs)
+  c4x15n      r5: C4 with its first read after 15 % returning 7, a value never written: invalid,
+              so the team stops mid-history
   c5xx2       c5x (the 1M-op counter, width 20: the counter closure tables) perturbed at 2 %
 
 Each is checked once by the oracle on the build container's CPU (one thread, as Knossos searches
@@ -43,6 +47,20 @@ from lincheck import synth  # noqa: E402
 RAMP_SEED0 = 0x5EED4000  # tools/crash_ramp.py SEED0 (SURVEY §8(d) seeds, config 4)
 
 
+def read_never_written(h, at_frac: float):
+    """h with its first :ok scalar read from entry at_frac * n returning 7, a value the register
+    generator never writes (its domain is 0..4): invalid at that read, so the search stops there."""
+    import numpy as np
+    from lincheck import history as H
+    t, f, vf = np.asarray(h.type), np.asarray(h.f), np.asarray(h.vflags)
+    start = int(at_frac * h.n)
+    j = start + int(np.nonzero((t[start:] == 1) & (f[start:] == 0) & (vf[start:] == H.V_SCALAR))[0][0])
+    v0 = np.array(h.v0, copy=True)
+    v0[j] = 7
+    return H.from_columns(np.array(h.index, copy=True), np.array(h.process, copy=True), t.copy(), f.copy(), v0,
+                          np.array(h.v1, copy=True), vf.copy())
+
+
 def ramp(k: int):
     return synth.gen_register(2000, 16, 0.002, RAMP_SEED0 + k, n_crashed=k)
 
@@ -69,6 +87,8 @@ GEN = {
                   lambda: synth.perturb_read(ramp(13), 0.5, "cas-register", 50)),
     "c4x15": ("cas-register", "synth.perturb_read(synth.gen_config('c4'), 0.15, 'cas-register', 15)",
               lambda: synth.perturb_read(synth.gen_config("c4"), 0.15, "cas-register", 15)),
+    "c4x15n": ("cas-register", "read_never_written(synth.gen_config('c4'), 0.15)",
+               lambda: read_never_written(synth.gen_config("c4"), 0.15)),
     "c5xx2": ("counter", "synth.perturb_read(synth.gen_config('c5x'), 0.02, 'counter', 2)",
               lambda: synth.perturb_read(synth.gen_config("c5x"), 0.02, "counter", 2)),
 }

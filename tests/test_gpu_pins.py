@@ -25,7 +25,7 @@ import pin_wide  # noqa: E402
 # the kernel each fixture must take (lc_check_stats counters)
 PATH = {"ramp11s": "wide_histories", "ramp10c17": "wide_histories", "ramp11c17": "wide_histories",
         "ramp13": "wide_histories", "ramp14": "wide_histories", "ramp16": "wide_histories",
-        "ramp13x50": "wide_histories", "c4x15": "dense_histories", "c5xx2": "ctab_histories"}
+        "ramp13x50": "wide_histories", "c4x15": "dense_histories", "c4x15n": "dense_histories", "c5xx2": "ctab_histories"}
 PINNED = [n for n in pin_wide.GEN if os.path.exists(pin_wide.path_of(n))]
 
 
